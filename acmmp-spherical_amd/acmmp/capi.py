@@ -1,0 +1,202 @@
+"""ctypes binding of the C ABI in include/acmmp.h (libacmmp.so, built in-tree for gfx950).
+
+This is the Python-side FFI a maintainer would add next to the reference;
+tests and bench.py drive the engine only through it.  There is no fallback: if the HIP
+library is missing or no GPU is visible, every call fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from .types import CAMERA_DTYPE, PARAMS_DTYPE
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libacmmp.so")
+
+STATUS = {0: "ok", 1: "invalid argument", 2: "HIP runtime error", 3: "out of device memory",
+          4: "call order violated", 5: "unsupported configuration", 6: "no HIP device"}
+
+# Every symbol include/acmmp.h declares (checked against the header by tests/test_capi_exports.py).
+EXPORTS = [
+    "acmmp_abi_version", "acmmp_create", "acmmp_destroy", "acmmp_status_str", "acmmp_last_error",
+    "acmmp_set_params", "acmmp_upload_views", "acmmp_upload_depths", "acmmp_set_state",
+    "acmmp_set_scaled_state", "acmmp_set_planar_prior", "acmmp_run_patchmatch", "acmmp_run_patchmatch_ex",
+    "acmmp_download", "acmmp_download_aux", "acmmp_device_outputs", "acmmp_last_timing", "acmmp_jbu",
+    "acmmp_debug_ncc", "acmmp_debug_geom",
+]
+
+
+class AcmmpError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libacmmp.so (no GPU needed to load it)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise AcmmpError(f"{path} is missing: build it with `python acmmp-spherical_amd/build.py` "
+                         "(there is no CPU fallback)")
+    L = C.CDLL(path)
+    vp, i32, u64 = C.c_void_p, C.c_int, C.c_uint64
+    L.acmmp_abi_version.restype = i32
+    L.acmmp_create.argtypes = [i32, C.POINTER(vp)]
+    L.acmmp_destroy.argtypes = [vp]
+    L.acmmp_destroy.restype = None
+    L.acmmp_status_str.argtypes = [i32]
+    L.acmmp_status_str.restype = C.c_char_p
+    L.acmmp_last_error.argtypes = [vp]
+    L.acmmp_last_error.restype = C.c_char_p
+    L.acmmp_set_params.argtypes = [vp, vp]
+    L.acmmp_upload_views.argtypes = [vp, i32, vp, vp, vp]
+    L.acmmp_upload_depths.argtypes = [vp, i32, vp, vp, vp]
+    L.acmmp_set_state.argtypes = [vp, vp, vp]
+    L.acmmp_set_scaled_state.argtypes = [vp, vp, i32, i32]
+    L.acmmp_set_planar_prior.argtypes = [vp, vp, vp]
+    L.acmmp_run_patchmatch.argtypes = [vp, u64]
+    L.acmmp_run_patchmatch_ex.argtypes = [vp, u64, i32, i32]
+    L.acmmp_download.argtypes = [vp, vp, vp]
+    L.acmmp_download_aux.argtypes = [vp, vp, vp]
+    L.acmmp_device_outputs.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
+    L.acmmp_last_timing.argtypes = [vp, vp]
+    L.acmmp_jbu.argtypes = [vp, vp, i32, i32, vp, i32, i32, i32, vp]
+    L.acmmp_debug_ncc.argtypes = [vp, i32, vp, vp, vp, vp]
+    L.acmmp_debug_geom.argtypes = [vp, i32, vp, vp, vp, vp]
+    for name in EXPORTS:
+        fn = getattr(L, name)
+        if name not in ("acmmp_destroy", "acmmp_status_str", "acmmp_last_error", "acmmp_abi_version"):
+            fn.restype = i32
+    _lib = L
+    return L
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Context:
+    """One reference-view problem on one GPU -- the device side of the reference's ACMMP object."""
+
+    def __init__(self, device: int = 0):
+        self.L = load_library()
+        h = C.c_void_p()
+        rc = self.L.acmmp_create(device, C.byref(h))
+        if rc != 0:
+            raise AcmmpError(f"acmmp_create({device}) failed: {STATUS.get(rc, rc)}")
+        self.h = h
+        self.W = self.H = self.N = 0
+        self._params = None
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.L.acmmp_last_error(self.h).decode()
+            raise AcmmpError(f"{what}: {STATUS.get(rc, rc)}: {msg}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.acmmp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- setup
+    def set_params(self, params):
+        p = np.frombuffer(np.asarray(params, dtype=PARAMS_DTYPE).tobytes(), np.uint8).copy()
+        self._params = p
+        self._check(self.L.acmmp_set_params(self.h, _p(p)), "set_params")
+
+    def upload_views(self, images, cameras):
+        imgs = [np.ascontiguousarray(im, np.float32) for im in images]
+        cams = np.frombuffer(np.ascontiguousarray(cameras, dtype=CAMERA_DTYPE).tobytes(), CAMERA_DTYPE).copy()
+        n = len(imgs)
+        ptrs = (C.c_void_p * n)(*[im.ctypes.data for im in imgs])
+        self._check(self.L.acmmp_upload_views(self.h, n, C.cast(ptrs, C.c_void_p), None, _p(cams)), "upload_views")
+        self.N, self.H, self.W = n, imgs[0].shape[0], imgs[0].shape[1]
+
+    def upload_depths(self, depths):
+        ds = [np.ascontiguousarray(d, np.float32) for d in depths]
+        n = len(ds)
+        ptrs = (C.c_void_p * n)(*[d.ctypes.data for d in ds])
+        w = np.array([d.shape[1] for d in ds], np.int32)
+        h = np.array([d.shape[0] for d in ds], np.int32)
+        self._check(self.L.acmmp_upload_depths(self.h, n, C.cast(ptrs, C.c_void_p), _p(w), _p(h)), "upload_depths")
+
+    def set_state(self, planes=None, costs=None):
+        pl = None if planes is None else np.ascontiguousarray(planes, np.float32)
+        co = None if costs is None else np.ascontiguousarray(costs, np.float32)
+        self._check(self.L.acmmp_set_state(self.h, _p(pl), _p(co)), "set_state")
+
+    def set_scaled_state(self, planes):
+        pl = np.ascontiguousarray(planes, np.float32)
+        self._check(self.L.acmmp_set_scaled_state(self.h, _p(pl), pl.shape[1], pl.shape[0]), "set_scaled_state")
+
+    def set_planar_prior(self, prior_planes, masks):
+        pr = np.ascontiguousarray(prior_planes, np.float32)
+        mk = np.ascontiguousarray(masks, np.uint32)
+        self._check(self.L.acmmp_set_planar_prior(self.h, _p(pr), _p(mk)), "set_planar_prior")
+
+    # -- run
+    def run_patchmatch(self, seed: int, n_half_sweeps: int = -1, do_post: bool = True):
+        self._check(self.L.acmmp_run_patchmatch_ex(self.h, C.c_uint64(seed), n_half_sweeps, int(do_post)),
+                    "run_patchmatch")
+
+    def download(self):
+        planes = np.empty((self.H, self.W, 4), np.float32)
+        costs = np.empty((self.H, self.W), np.float32)
+        self._check(self.L.acmmp_download(self.h, _p(planes), _p(costs)), "download")
+        return planes, costs
+
+    def download_aux(self):
+        sel = np.empty((self.H, self.W), np.uint32)
+        pre = np.empty((self.H, self.W), np.float32)
+        self._check(self.L.acmmp_download_aux(self.h, _p(sel), _p(pre)), "download_aux")
+        return sel, pre
+
+    def device_outputs(self):
+        a, b = C.c_void_p(), C.c_void_p()
+        self._check(self.L.acmmp_device_outputs(self.h, C.byref(a), C.byref(b)), "device_outputs")
+        return a.value, b.value
+
+    def last_timing(self):
+        ms = np.zeros(3, np.float32)
+        self._check(self.L.acmmp_last_timing(self.h, _p(ms)), "last_timing")
+        return {"init_ms": float(ms[0]), "prop_ms": float(ms[1]), "post_ms": float(ms[2])}
+
+    def jbu(self, ref, coarse, imagescale: int):
+        ref = np.ascontiguousarray(ref, np.float32)
+        coarse = np.ascontiguousarray(coarse, np.float32)
+        out = np.empty_like(ref)
+        self._check(self.L.acmmp_jbu(self.h, _p(ref), ref.shape[1], ref.shape[0], _p(coarse), coarse.shape[1],
+                                     coarse.shape[0], imagescale, _p(out)), "jbu")
+        return out
+
+    def _debug(self, fn, px, py, planes):
+        px = np.ascontiguousarray(px, np.int32)
+        py = np.ascontiguousarray(py, np.int32)
+        pl = np.ascontiguousarray(planes, np.float32).reshape(-1, 4)
+        out = np.empty((len(px), self.N - 1), np.float32)
+        self._check(fn(self.h, len(px), _p(px), _p(py), _p(pl), _p(out)), "debug")
+        return out
+
+    def debug_ncc(self, px, py, planes):
+        return self._debug(self.L.acmmp_debug_ncc, px, py, planes)
+
+    def debug_geom(self, px, py, planes):
+        return self._debug(self.L.acmmp_debug_geom, px, py, planes)

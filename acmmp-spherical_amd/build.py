@@ -1,0 +1,55 @@
+"""Build the in-tree HIP extension libacmmp.so for gfx950 (no cmake; plain hipcc).
+
+`python acmmp-spherical_amd/build.py` or `acmmp.build.build()`; __graft_entry__.build()
+calls it.  Objects are rebuilt only when a source or header is newer than the .so.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+LIB = os.path.join(HERE, "acmmp", "libacmmp.so")
+ARCH = os.environ.get("ACMMP_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+SOURCES = ["kernels.hip", "capi.cpp"]
+HEADERS = ["engine.h", "detmath.h"]
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}",
+          f"-I{INCLUDE}", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
+
+
+def _newest(paths):
+    return max(os.path.getmtime(p) for p in paths)
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(INCLUDE, "acmmp.h")]
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest(deps):
+        return LIB
+    objdir = os.path.join(HERE, "build")
+    os.makedirs(objdir, exist_ok=True)
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(objdir, src + ".o")
+        srcp = os.path.join(CSRC, src)
+        hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "acmmp.h")]
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < _newest([srcp] + hdrs):
+            lang = ["-x", "hip"] if src.endswith(".cpp") else []
+            cmd = [HIPCC, *COMMON, *lang, "-c", srcp, "-o", obj]
+            if verbose:
+                print("[acmmp build]", " ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+        objs.append(obj)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+    if verbose:
+        print("[acmmp build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,546 @@
+// capi.cpp -- implementation of include/acmmp.h (the drop-in boundary).
+//
+// Owns every device buffer of one reference-view problem, like the reference's ACMMP
+// object (ACMMP.h:82-111), and sequences the kernels of ACMMP::RunPatchMatch
+// (ACMMP.cu:1506-1556) on one HIP stream.  No OpenCV, no textures: images live in
+// plain padded fp32 buffers (engine.h).
+#include "../../include/acmmp.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+
+using namespace acmmp;
+
+static_assert(sizeof(acmmp_camera) == 120, "Camera layout (main.h:189-203)");
+static_assert(sizeof(acmmp_params) == 68, "PatchMatchParams layout (ACMMP.h:32-55)");
+static_assert(offsetof(acmmp_params, scaled_cols) == 52, "PatchMatchParams layout");
+static_assert(offsetof(acmmp_params, geom_consistency) == 60, "PatchMatchParams layout");
+
+struct acmmp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    acmmp_params params{};
+    bool has_params = false;
+
+    int N = 0, W = 0, H = 0, model = -1;
+    std::vector<acmmp_camera> cams;
+    std::vector<DevCam> dcams;
+    DevCam* d_cams = nullptr;
+    float* d_img = nullptr;
+
+    float* d_dep = nullptr;
+    bool has_depths = false;
+
+    float4* d_dirs = nullptr;
+    int dirs_R = -1;
+
+    float* d_tw = nullptr;
+    float* d_twr = nullptr;
+    float* d_tr = nullptr;
+    float* d_tsum = nullptr;
+    size_t table_S = 0;
+
+    float4* d_planes_rm = nullptr;
+    float* d_costs_rm = nullptr;
+    float* d_pre = nullptr;
+    uint32_t* d_sel_rm = nullptr;
+
+    float4* d_scaled = nullptr;
+    int sw = 0, sh = 0;
+
+    float4* d_prior = nullptr;
+    uint32_t* d_mask = nullptr;
+
+    float4* d_plane_cs[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    float* d_cost_cs[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    uint32_t* d_sel_cs[2] = {nullptr, nullptr};
+    uint32_t* d_rng_cs[2] = {nullptr, nullptr};
+    float* d_scratch = nullptr;
+    size_t scratch_V = 0;
+
+    float timing[3] = {0.f, 0.f, 0.f};
+    std::string err;
+};
+
+namespace {
+
+acmmp_status fail(acmmp_ctx* c, acmmp_status s, const std::string& msg) {
+    if (c) c->err = msg;
+    return s;
+}
+
+#define HIP_TRY(ctx, expr)                                                                         \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            return fail((ctx), e_ == hipErrorOutOfMemory ? ACMMP_ERR_OUT_OF_MEMORY : ACMMP_ERR_HIP, \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                        \
+        }                                                                                          \
+    } while (0)
+
+template <typename T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+template <typename T>
+hipError_t dalloc(T*& p, size_t count) {
+    dfree(p);
+    return hipMalloc(reinterpret_cast<void**>(&p), sizeof(T) * std::max<size_t>(count, 1));
+}
+
+size_t P_of(const acmmp_ctx* c) { return static_cast<size_t>(c->W) * c->H; }
+int Wh_of(const acmmp_ctx* c) { return (c->W + 1) / 2; }
+
+// Camera centre exactly as Get3DPointonWorld_cu rounds it (ACMMP.cu:592-594), fused like the kernels.
+float neg_dot3(float a0, float a1, float a2, float b0, float b1, float b2) {
+    return -std::fmaf(a2, b2, std::fmaf(a1, b1, a0 * b0));
+}
+
+}  // namespace
+
+extern "C" {
+
+int acmmp_abi_version(void) { return ACMMP_ABI_VERSION; }
+
+const char* acmmp_status_str(acmmp_status s) {
+    switch (s) {
+    case ACMMP_OK: return "ok";
+    case ACMMP_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case ACMMP_ERR_HIP: return "HIP runtime error";
+    case ACMMP_ERR_OUT_OF_MEMORY: return "out of device memory";
+    case ACMMP_ERR_STATE: return "call order violated";
+    case ACMMP_ERR_UNSUPPORTED: return "unsupported configuration";
+    case ACMMP_ERR_NO_DEVICE: return "no HIP device";
+    }
+    return "unknown status";
+}
+
+const char* acmmp_last_error(const acmmp_ctx* ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+acmmp_status acmmp_create(int device, acmmp_ctx** out) {
+    if (!out) return ACMMP_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ACMMP_ERR_NO_DEVICE;
+    if (device >= n) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (device < 0) {
+        if (hipGetDevice(&device) != hipSuccess) return ACMMP_ERR_HIP;
+    }
+    if (hipSetDevice(device) != hipSuccess) return ACMMP_ERR_HIP;
+    acmmp_ctx* c = new acmmp_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return ACMMP_ERR_HIP;
+    }
+    for (auto& e : c->ev) {
+        if (hipEventCreate(&e) != hipSuccess) {
+            acmmp_destroy(c);
+            return ACMMP_ERR_HIP;
+        }
+    }
+    *out = c;
+    return ACMMP_OK;
+}
+
+void acmmp_destroy(acmmp_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    dfree(c->d_cams); dfree(c->d_img); dfree(c->d_dep); dfree(c->d_dirs);
+    dfree(c->d_tw); dfree(c->d_twr); dfree(c->d_tr); dfree(c->d_tsum);
+    dfree(c->d_planes_rm); dfree(c->d_costs_rm); dfree(c->d_pre); dfree(c->d_sel_rm);
+    dfree(c->d_scaled); dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_scratch);
+    for (int k = 0; k < 2; ++k) {
+        for (int b = 0; b < 2; ++b) { dfree(c->d_plane_cs[k][b]); dfree(c->d_cost_cs[k][b]); }
+        dfree(c->d_sel_cs[k]); dfree(c->d_rng_cs[k]);
+    }
+    for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+acmmp_status acmmp_set_params(acmmp_ctx* c, const acmmp_params* p) {
+    if (!c || !p) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
+    if (p->num_images < 2 || p->num_images > kMaxViews + 1)
+        return fail(c, ACMMP_ERR_UNSUPPORTED, "num_images must be in [2, 33] (32 source views max)");
+    if (p->patch_size < 1 || p->radius_increment < 1 || p->top_k < 0 || p->max_iterations < 0)
+        return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "invalid patch_size/radius_increment/top_k/max_iterations");
+    c->params = *p;
+    c->has_params = true;
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images, const size_t* pitch_bytes,
+                                const acmmp_camera* cams) {
+    if (!c || !images || !cams) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
+    if (n < 2 || n > kMaxViews + 1) return fail(c, ACMMP_ERR_UNSUPPORTED, "need 2..33 images");
+    for (int i = 0; i < n; ++i) {
+        if (!images[i] || cams[i].width <= 0 || cams[i].height <= 0 || cams[i].width > 32767 || cams[i].height > 32767)
+            return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "bad image " + std::to_string(i));
+        if (cams[i].model != ACMMP_PINHOLE && cams[i].model != ACMMP_SPHERE)
+            return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "unknown camera model");
+        if (cams[i].model != cams[0].model)
+            return fail(c, ACMMP_ERR_UNSUPPORTED, "mixed camera models in one problem are not supported");
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    const bool resized = (c->W != cams[0].width || c->H != cams[0].height);
+    c->N = n;
+    c->W = cams[0].width;
+    c->H = cams[0].height;
+    c->model = cams[0].model;
+    c->cams.assign(cams, cams + n);
+    c->dirs_R = -1;
+
+    // padded images in one allocation
+    std::vector<long long> off(n);
+    long long total = 0;
+    for (int i = 0; i < n; ++i) {
+        off[i] = total;                                 // base = padded texel (-1,-1)
+        total += static_cast<long long>(cams[i].width + 2) * (cams[i].height + 2);
+        total = (total + 63) & ~63LL;
+    }
+    HIP_TRY(c, dalloc(c->d_img, static_cast<size_t>(total)));
+    float* staging = nullptr;
+    size_t staging_cap = 0;
+    for (int i = 0; i < n; ++i) {
+        const size_t rowb = sizeof(float) * cams[i].width;
+        const size_t pb = pitch_bytes ? pitch_bytes[i] : rowb;
+        const size_t bytes = pb * (cams[i].height - 1) + rowb;
+        if (bytes > staging_cap) {
+            dfree(staging);
+            HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&staging), bytes));
+            staging_cap = bytes;
+        }
+        HIP_TRY(c, hipMemcpyAsync(staging, images[i], bytes, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, launch_pad_image(staging, pb / sizeof(float), cams[i].width, cams[i].height, c->d_img + off[i],
+                                    cams[i].width + 2, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    dfree(staging);
+
+    c->dcams.assign(n, DevCam{});
+    for (int i = 0; i < n; ++i) {
+        const acmmp_camera& s = cams[i];
+        DevCam& d = c->dcams[i];
+        d.model = s.model; d.W = s.width; d.H = s.height; d.img_pitch = s.width + 2;
+        std::memcpy(d.R, s.R, sizeof d.R);
+        std::memcpy(d.t, s.t, sizeof d.t);
+        std::memcpy(d.K, s.K, sizeof d.K);
+        d.cx = s.params[1]; d.cy = s.params[2];
+        d.inv_fx = 1.0f / s.K[0];
+        d.inv_fy = 1.0f / s.K[4];
+        d.invW = 1.0f / static_cast<float>(s.width);
+        d.Wf = static_cast<float>(s.width);
+        d.Hf = static_cast<float>(s.height);
+        d.C[0] = neg_dot3(s.R[0], s.R[3], s.R[6], s.t[0], s.t[1], s.t[2]);
+        d.C[1] = neg_dot3(s.R[1], s.R[4], s.R[7], s.t[0], s.t[1], s.t[2]);
+        d.C[2] = neg_dot3(s.R[2], s.R[5], s.R[8], s.t[0], s.t[1], s.t[2]);
+        d.img_off = off[i];
+        d.dep_off = 0; d.dep_w = 1; d.dep_h = 1;
+    }
+    HIP_TRY(c, dalloc(c->d_cams, static_cast<size_t>(n)));
+    HIP_TRY(c, hipMemcpy(c->d_cams, c->dcams.data(), sizeof(DevCam) * n, hipMemcpyHostToDevice));
+    c->has_depths = false;
+
+    if (resized || !c->d_planes_rm) {
+        const size_t P = P_of(c);
+        const size_t Pc = static_cast<size_t>(c->H) * Wh_of(c);
+        HIP_TRY(c, dalloc(c->d_planes_rm, P));
+        HIP_TRY(c, dalloc(c->d_costs_rm, P));
+        HIP_TRY(c, dalloc(c->d_pre, P));
+        HIP_TRY(c, dalloc(c->d_sel_rm, P));
+        HIP_TRY(c, hipMemset(c->d_planes_rm, 0, sizeof(float4) * P));
+        HIP_TRY(c, hipMemset(c->d_costs_rm, 0, sizeof(float) * P));
+        HIP_TRY(c, hipMemset(c->d_pre, 0, sizeof(float) * P));   // never written outside the upsample branch
+        HIP_TRY(c, hipMemset(c->d_sel_rm, 0, sizeof(uint32_t) * P));
+        for (int k = 0; k < 2; ++k) {
+            for (int b = 0; b < 2; ++b) {
+                HIP_TRY(c, dalloc(c->d_plane_cs[k][b], Pc));
+                HIP_TRY(c, dalloc(c->d_cost_cs[k][b], Pc));
+            }
+            HIP_TRY(c, dalloc(c->d_sel_cs[k], Pc));
+            HIP_TRY(c, dalloc(c->d_rng_cs[k], Pc));
+        }
+        dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_tw); dfree(c->d_twr); dfree(c->d_tr); dfree(c->d_tsum);
+        dfree(c->d_scratch);
+        c->table_S = 0;
+        c->scratch_V = 0;
+    }
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_upload_depths(acmmp_ctx* c, int n, const float* const* depths, const int* w, const int* h) {
+    if (!c || !depths || !w || !h) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
+    if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
+    if (n < c->N) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "need one depth map per image");
+    HIP_TRY(c, hipSetDevice(c->device));
+    size_t total = 0;
+    std::vector<size_t> off(c->N);
+    for (int i = 0; i < c->N; ++i) {
+        if (!depths[i] || w[i] <= 0 || h[i] <= 0) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "bad depth map");
+        off[i] = total;
+        total += static_cast<size_t>(w[i]) * h[i];
+    }
+    HIP_TRY(c, dalloc(c->d_dep, total));
+    for (int i = 0; i < c->N; ++i) {
+        HIP_TRY(c, hipMemcpy(c->d_dep + off[i], depths[i], sizeof(float) * w[i] * h[i], hipMemcpyHostToDevice));
+        c->dcams[i].dep_off = static_cast<long long>(off[i]);
+        c->dcams[i].dep_w = w[i];
+        c->dcams[i].dep_h = h[i];
+    }
+    HIP_TRY(c, hipMemcpy(c->d_cams, c->dcams.data(), sizeof(DevCam) * c->N, hipMemcpyHostToDevice));
+    c->has_depths = true;
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_set_state(acmmp_ctx* c, const float* planes, const float* costs) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t P = P_of(c);
+    if (planes) HIP_TRY(c, hipMemcpy(c->d_planes_rm, planes, sizeof(float4) * P, hipMemcpyHostToDevice));
+    if (costs) HIP_TRY(c, hipMemcpy(c->d_costs_rm, costs, sizeof(float) * P, hipMemcpyHostToDevice));
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_set_scaled_state(acmmp_ctx* c, const float* planes, int sw, int sh) {
+    if (!c || !planes || sw <= 0 || sh <= 0) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "bad scaled state");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, dalloc(c->d_scaled, static_cast<size_t>(sw) * sh));
+    HIP_TRY(c, hipMemcpy(c->d_scaled, planes, sizeof(float4) * sw * sh, hipMemcpyHostToDevice));
+    c->sw = sw;
+    c->sh = sh;
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_set_planar_prior(acmmp_ctx* c, const float* prior, const uint32_t* masks) {
+    if (!c || !prior || !masks) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
+    if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t P = P_of(c);
+    HIP_TRY(c, dalloc(c->d_prior, P));
+    HIP_TRY(c, dalloc(c->d_mask, P));
+    HIP_TRY(c, hipMemcpy(c->d_prior, prior, sizeof(float4) * P, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(c->d_mask, masks, sizeof(uint32_t) * P, hipMemcpyHostToDevice));
+    return ACMMP_OK;
+}
+
+static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
+    const acmmp_params& p = c->params;
+    if (!c->has_params) return fail(c, ACMMP_ERR_STATE, "set_params first");
+    if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
+    if (p.num_images != c->N) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "params.num_images != uploaded images");
+    if (p.geom_consistency && !c->has_depths) return fail(c, ACMMP_ERR_STATE, "geom_consistency needs upload_depths");
+    if (p.planar_prior && (!c->d_prior || !c->d_mask)) return fail(c, ACMMP_ERR_STATE, "planar_prior needs set_planar_prior");
+    if (!p.geom_consistency && p.hierarchy && !p.planar_prior && !c->d_scaled)
+        return fail(c, ACMMP_ERR_STATE, "hierarchy needs set_scaled_state");
+    if (p.upsample && !p.planar_prior && p.hierarchy &&
+        (c->sw != static_cast<int>(p.scaled_cols) || c->sh != static_cast<int>(p.scaled_rows)))
+        return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "scaled_cols/rows != scaled state size");
+    if (p.hierarchy && !p.upsample && !p.geom_consistency && !p.planar_prior && (c->sw != c->W || c->sh != c->H))
+        return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "hierarchy reuse needs a full-size scaled state");
+    const int R = p.patch_size / 2;
+    if (R > 64) return fail(c, ACMMP_ERR_UNSUPPORTED, "patch radius > 64");
+    int nside = 0;
+    for (int i = -R; i <= R; i += p.radius_increment) ++nside;
+    kp = KParams{};
+    kp.model = c->model;
+    kp.W = c->W; kp.H = c->H; kp.Wh = Wh_of(c); kp.N = c->N; kp.V = c->N - 1;
+    kp.R = R; kp.inc = p.radius_increment; kp.nside = nside; kp.S = nside * nside;
+    kp.rows = std::min(c->H, 32 * (((c->H / 2) + 15) / 16));
+    kp.dpitch = c->W + 2 * R;
+    kp.depth_min = p.depth_min; kp.depth_max = p.depth_max;
+    kp.sigma_spatial = p.sigma_spatial; kp.sigma_color = p.sigma_color;
+    kp.top_k = p.top_k;
+    kp.geom = p.geom_consistency; kp.planar = p.planar_prior; kp.hier = p.hierarchy; kp.upsample = p.upsample;
+    kp.scaled_cols = p.scaled_cols; kp.scaled_rows = p.scaled_rows;
+    kp.sw = c->sw; kp.sh = c->sh;
+    kp.seed_lo = static_cast<uint32_t>(seed);
+    kp.seed_hi = static_cast<uint32_t>(seed >> 32);
+    kp.Pc = static_cast<long long>(c->H) * kp.Wh;
+    const size_t Pc = static_cast<size_t>(kp.Pc);
+
+    if (c->dirs_R != R) {
+        HIP_TRY(c, dalloc(c->d_dirs, static_cast<size_t>(c->W + 2 * R) * (c->H + 2 * R)));
+        kp.cams = c->d_cams;
+        HIP_TRY(c, launch_dir_table(kp, c->d_dirs, c->stream));
+        c->dirs_R = R;
+    }
+    if (c->table_S != static_cast<size_t>(kp.S)) {
+        HIP_TRY(c, dalloc(c->d_tw, 2 * kp.S * Pc));
+        HIP_TRY(c, dalloc(c->d_twr, 2 * kp.S * Pc));
+        HIP_TRY(c, dalloc(c->d_tr, 2 * kp.S * Pc));
+        HIP_TRY(c, dalloc(c->d_tsum, 3 * 2 * Pc));
+        c->table_S = kp.S;
+    }
+    if (c->scratch_V != static_cast<size_t>(kp.V)) {
+        HIP_TRY(c, dalloc(c->d_scratch, 8 * static_cast<size_t>(kp.V) * Pc));
+        c->scratch_V = kp.V;
+    }
+    kp.cams = c->d_cams;
+    kp.img = c->d_img;
+    kp.dep = c->d_dep;
+    kp.dirs = c->d_dirs;
+    kp.tw = c->d_tw; kp.twr = c->d_twr; kp.tr = c->d_tr; kp.tsum = c->d_tsum;
+    kp.planes_rm = c->d_planes_rm; kp.costs_rm = c->d_costs_rm; kp.pre_rm = c->d_pre; kp.sel_rm = c->d_sel_rm;
+    kp.scaled = c->d_scaled; kp.prior = c->d_prior; kp.mask = c->d_mask;
+    for (int k = 0; k < 2; ++k) {
+        kp.plane_cs[k] = c->d_plane_cs[k][0];
+        kp.cost_cs[k] = c->d_cost_cs[k][0];
+        kp.sel_cs[k] = c->d_sel_cs[k];
+        kp.rng_cs[k] = c->d_rng_cs[k];
+    }
+    kp.scratch = c->d_scratch;
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx* c, uint64_t seed, int n_half_sweeps, int do_post) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    HIP_TRY(c, hipSetDevice(c->device));
+    KParams kp;
+    acmmp_status st = build_kparams(c, kp, seed);
+    if (st != ACMMP_OK) return st;
+    if (n_half_sweeps < 0) n_half_sweeps = 2 * c->params.max_iterations;
+    const size_t Pc = static_cast<size_t>(kp.Pc);
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipEventRecord(c->ev[0], s));
+    HIP_TRY(c, launch_prepare(kp, s));
+    HIP_TRY(c, launch_init(kp, s));
+    // rows outside the reference's checkerboard grid are never rewritten: keep both buffers equal
+    int cur[2] = {0, 0};
+    for (int k = 0; k < 2; ++k) {
+        HIP_TRY(c, hipMemcpyAsync(c->d_plane_cs[k][1], c->d_plane_cs[k][0], sizeof(float4) * Pc,
+                                  hipMemcpyDeviceToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(c->d_cost_cs[k][1], c->d_cost_cs[k][0], sizeof(float) * Pc,
+                                  hipMemcpyDeviceToDevice, s));
+    }
+    HIP_TRY(c, hipEventRecord(c->ev[1], s));
+    for (int sw = 0; sw < n_half_sweeps; ++sw) {
+        const int colour = sw & 1, iter = sw / 2;
+        SweepOut out{c->d_plane_cs[colour][cur[colour] ^ 1], c->d_cost_cs[colour][cur[colour] ^ 1]};
+        HIP_TRY(c, launch_propagate(kp, colour, iter, out, s));
+        cur[colour] ^= 1;
+        kp.plane_cs[colour] = c->d_plane_cs[colour][cur[colour]];
+        kp.cost_cs[colour] = c->d_cost_cs[colour][cur[colour]];
+    }
+    HIP_TRY(c, hipEventRecord(c->ev[2], s));
+    HIP_TRY(c, launch_post(kp, do_post, s));
+    HIP_TRY(c, hipEventRecord(c->ev[3], s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    // keep buffer 0 current for the next run
+    for (int k = 0; k < 2; ++k) {
+        if (cur[k]) {
+            std::swap(c->d_plane_cs[k][0], c->d_plane_cs[k][1]);
+            std::swap(c->d_cost_cs[k][0], c->d_cost_cs[k][1]);
+        }
+    }
+    for (int i = 0; i < 3; ++i) HIP_TRY(c, hipEventElapsedTime(&c->timing[i], c->ev[i], c->ev[i + 1]));
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_run_patchmatch(acmmp_ctx* c, uint64_t seed) { return acmmp_run_patchmatch_ex(c, seed, -1, 1); }
+
+acmmp_status acmmp_download(acmmp_ctx* c, float* planes, float* costs) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "nothing to download");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t P = P_of(c);
+    if (planes) HIP_TRY(c, hipMemcpy(planes, c->d_planes_rm, sizeof(float4) * P, hipMemcpyDeviceToHost));
+    if (costs) HIP_TRY(c, hipMemcpy(costs, c->d_costs_rm, sizeof(float) * P, hipMemcpyDeviceToHost));
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_download_aux(acmmp_ctx* c, uint32_t* sel, float* pre) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "nothing to download");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t P = P_of(c);
+    if (sel) HIP_TRY(c, hipMemcpy(sel, c->d_sel_rm, sizeof(uint32_t) * P, hipMemcpyDeviceToHost));
+    if (pre) HIP_TRY(c, hipMemcpy(pre, c->d_pre, sizeof(float) * P, hipMemcpyDeviceToHost));
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_device_outputs(acmmp_ctx* c, void** planes, void** costs) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (planes) *planes = c->d_planes_rm;
+    if (costs) *costs = c->d_costs_rm;
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_last_timing(const acmmp_ctx* c, float ms[3]) {
+    if (!c || !ms) return ACMMP_ERR_INVALID_ARGUMENT;
+    for (int i = 0; i < 3; ++i) ms[i] = c->timing[i];
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_jbu(acmmp_ctx* c, const float* ref, int W, int H, const float* coarse, int sw, int sh,
+                       int imagescale, float* out) {
+    if (!c || !ref || !coarse || !out || W <= 0 || H <= 0 || sw <= 0 || sh <= 0 || imagescale < 0)
+        return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "bad JBU arguments");
+    HIP_TRY(c, hipSetDevice(c->device));
+    float *d_ref = nullptr, *d_coarse = nullptr, *d_out = nullptr;
+    const size_t P = static_cast<size_t>(W) * H, p = static_cast<size_t>(sw) * sh;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&d_ref), sizeof(float) * P);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_coarse), sizeof(float) * p);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_out), sizeof(float) * P);
+    if (e == hipSuccess) e = hipMemcpy(d_ref, ref, sizeof(float) * P, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_coarse, coarse, sizeof(float) * p, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_jbu(d_ref, W, H, d_coarse, sw, sh, imagescale, d_out, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, sizeof(float) * P, hipMemcpyDeviceToHost);
+    dfree(d_ref); dfree(d_coarse); dfree(d_out);
+    if (e != hipSuccess) return fail(c, ACMMP_ERR_HIP, std::string("jbu: ") + hipGetErrorString(e));
+    return ACMMP_OK;
+}
+
+static acmmp_status debug_eval(acmmp_ctx* c, int which, int n, const int* px, const int* py, const float* planes,
+                               float* out) {
+    if (!c || !px || !py || !planes || !out || n <= 0) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "bad debug args");
+    HIP_TRY(c, hipSetDevice(c->device));
+    KParams kp;
+    acmmp_status st = build_kparams(c, kp, 0);
+    if (st != ACMMP_OK) return st;
+    for (int q = 0; q < n; ++q)
+        if (px[q] < 0 || py[q] < 0 || px[q] >= c->W || py[q] >= c->H)
+            return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "query pixel outside the reference image");
+    if (which == 1 && !c->has_depths) return fail(c, ACMMP_ERR_STATE, "geom cost needs upload_depths");
+    int *dx = nullptr, *dy = nullptr;
+    float4* dp = nullptr;
+    float* dout = nullptr;
+    const size_t nout = static_cast<size_t>(n) * kp.V;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&dx), sizeof(int) * n);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&dy), sizeof(int) * n);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&dp), sizeof(float4) * n);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&dout), sizeof(float) * nout);
+    if (e == hipSuccess) e = hipMemcpy(dx, px, sizeof(int) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dy, py, sizeof(int) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dp, planes, sizeof(float4) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_prepare(kp, c->stream);
+    if (e == hipSuccess) e = launch_debug(kp, which, n, dx, dy, dp, dout, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(float) * nout, hipMemcpyDeviceToHost);
+    dfree(dx); dfree(dy); dfree(dp); dfree(dout);
+    if (e != hipSuccess) return fail(c, ACMMP_ERR_HIP, std::string("debug: ") + hipGetErrorString(e));
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_debug_ncc(acmmp_ctx* c, int n, const int* px, const int* py, const float* planes, float* costs) {
+    return debug_eval(c, 0, n, px, py, planes, costs);
+}
+acmmp_status acmmp_debug_geom(acmmp_ctx* c, int n, const int* px, const int* py, const float* planes, float* out) {
+    return debug_eval(c, 1, n, px, py, planes, out);
+}
+
+}  // extern "C"

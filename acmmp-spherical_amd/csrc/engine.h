@@ -1,0 +1,95 @@
+// engine.h -- internal device-side layout of the PatchMatch engine (not part of the ABI).
+//
+// HBM layout:
+//  * source/reference images: one allocation, each view padded by one replicated
+//    texel on every side so a bilinear footprint is always two 8-byte row pairs;
+//  * reference ray table `dirs`: float4 per pixel of the reference view, padded by
+//    the patch radius (PixelToDir, ACMMP.cu:119-134, evaluated once per view
+//    instead of per sample);
+//  * per-pixel patch tables (bilateral weight w, w*ref, ref texel) colour-split,
+//    sample-major, so a wave reads them coalesced;
+//  * working state colour-split (black = (x+y) even, red = odd), each colour
+//    row-major over (H, ceil(W/2)); planes and costs double-buffered per colour so
+//    a half-sweep reads the kernel-entry snapshot of its own colour;
+//  * persistent state (what the reference keeps in plane_hypotheses_cuda /
+//    costs_cuda between runs) row-major.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace acmmp {
+
+constexpr int kPinhole = 0;
+constexpr int kSphere = 11;
+constexpr int kMaxViews = 32;       // cost_vector[32], uint32 view bitmask (ACMMP.cu:522,1153)
+
+struct DevCam {
+    int model, W, H, img_pitch;     // img_pitch: floats per padded row (W + 2)
+    float R[9];
+    float t[3];
+    float K[9];
+    float cx, cy;                   // SPHERE params[1], params[2]
+    float inv_fx, inv_fy;           // 1/K[0], 1/K[4]  (pinhole world point)
+    float invW;                     // 1/W             (SPHERE longitude wrap)
+    float Wf, Hf;
+    float C[3];                     // camera centre -(R^T t), computed like ACMMP.cu:592-594
+    long long img_off;              // float offset of padded texel (-1,-1)
+    long long dep_off;              // float offset of the geom depth map (row-major)
+    int dep_w, dep_h;
+};
+
+struct KParams {
+    int model;                      // kPinhole / kSphere, uniform over all views
+    int W, H, Wh, N, V;             // ref size, colour row width ceil(W/2), images, source views
+    int R, inc, nside, S;           // patch radius, radius_increment, offsets per axis, samples
+    int rows;                       // rows the reference's checkerboard grid covers
+    int dpitch;                     // dir table pitch (W + 2R)
+    float depth_min, depth_max, sigma_spatial, sigma_color;
+    int top_k;
+    int geom, planar, hier, upsample;
+    float scaled_cols, scaled_rows;
+    int sw, sh;
+    uint32_t seed_lo, seed_hi;
+    const DevCam* cams;
+    const float* img;
+    const float* dep;
+    const float4* dirs;
+    const float* tw;                // [2][S][Pc]  bilateral weight
+    const float* twr;               // [2][S][Pc]  weight * ref texel
+    const float* tr;                // [2][S][Pc]  ref texel
+    const float* tsum;              // [2][3][Pc]  SPHERE: sum_bw, sum_ref, sum_ref_ref
+    float4* planes_rm;              // persistent row-major state
+    float* costs_rm;
+    float* pre_rm;
+    uint32_t* sel_rm;
+    const float4* scaled;           // hierarchy coarse planes (sw x sh)
+    const float4* prior;            // planar prior planes (P)
+    const uint32_t* mask;           // planar prior labels (P)
+    float4* plane_cs[2];            // working state, current buffer per colour
+    float* cost_cs[2];
+    uint32_t* sel_cs[2];
+    uint32_t* rng_cs[2];            // Philox draw counter per pixel
+    float* scratch;                 // [8][V][Pc] propagation cost matrix
+    long long Pc;                   // H * Wh
+};
+
+// Per-half-sweep output buffers of the colour being updated.
+struct SweepOut {
+    float4* plane;
+    float* cost;
+};
+
+// Host-side launchers (kernels.hip).
+hipError_t launch_prepare(const KParams& kp, hipStream_t s);
+hipError_t launch_dir_table(const KParams& kp, float4* dirs, hipStream_t s);
+hipError_t launch_init(const KParams& kp, hipStream_t s);
+hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s);
+hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s);
+hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int sw, int sh, int imagescale,
+                      float* out, hipStream_t s);
+hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,
+                        float* out, hipStream_t s);
+hipError_t launch_pad_image(const float* src, size_t pitch_floats, int W, int H, float* dst, int dst_pitch,
+                            hipStream_t s);
+
+}  // namespace acmmp

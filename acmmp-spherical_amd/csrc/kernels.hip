@@ -1,0 +1,1235 @@
+// kernels.hip -- gfx950 kernels of the ACMMP-Spherical PatchMatch hot path.
+//
+// Reference: /root/reference/ACMMP.cu:14-1649 (RandomInitialization,
+// Black/RedPixelUpdate -> CheckerboardPropagation, GetDepthandNormal,
+// Black/RedPixelFilter, JBU_cu).  Semantics are those of DESIGN.md §2 (the
+// reference's algorithm with its undefined / non-reproducible parts fixed), and the
+// output is bit-identical to the CPU oracle (oracle/acmmp_oracle.c).
+//
+// Structure:
+//  * one lane per pixel of the colour being updated, 64x4 workgroups over the
+//    colour-split grid, so a wave owns 64 consecutive same-colour pixels of a row;
+//  * the 36-sample bilateral NCC is evaluated sample-outer / view-inner: the
+//    view-independent part of a sample (ray, plane depth, world point) is computed
+//    once and projected into a chunk of VB source views held in registers;
+//  * bilateral weights, w*ref and ref texels are per-pixel tables built once per
+//    run (they depend only on the reference image), so no exp() runs per sample;
+//  * current-hypothesis and refinement costs are evaluated only for views some
+//    lane of the wave selected (zero-weight views add exactly +0 in the reference).
+#include "detmath.h"
+#include "engine.h"
+
+namespace acmmp {
+
+// ------------------------------------------------------------------ RNG
+
+__device__ __forceinline__ uint4 philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                          uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+
+// curand_init(seed, subsequence = row-major pixel, 0) on a Philox4_32_10 state; uniform() = curand_uniform
+struct Rng {
+    uint32_t k0, k1, sub, n, blk_id;
+    uint4 blk;
+    __device__ __forceinline__ void init(uint32_t seed_lo, uint32_t seed_hi, uint32_t pixel, uint32_t count) {
+        k0 = seed_lo; k1 = seed_hi; sub = pixel; n = count; blk_id = 0xFFFFFFFFu;
+    }
+    __device__ __forceinline__ float uniform() {
+        const uint32_t b = n >> 2;
+        if (b != blk_id) { blk = philox10(b, 0u, sub, 0u, k0, k1); blk_id = b; }
+        const uint32_t w = n & 3u;
+        const uint32_t x = w == 0 ? blk.x : (w == 1 ? blk.y : (w == 2 ? blk.z : blk.w));
+        ++n;
+        return fmaf(static_cast<float>(x), 2.3283064365386963e-10f, 1.1641532182693481e-10f);
+    }
+};
+
+// ------------------------------------------------------------------ camera model
+
+__device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
+    const float inv = det_rsqrt(dot3(x, y, z, x, y, z));
+    x *= inv; y *= inv; z *= inv;
+}
+
+// PixelToDir, ACMMP.cu:119-134
+__device__ __forceinline__ float3 pixel_to_dir(const DevCam& c, int px, int py) {
+    float3 d;
+    if (c.model == kPinhole) {
+        d.x = (static_cast<float>(px) - c.K[2]) / c.K[0];
+        d.y = (static_cast<float>(py) - c.K[5]) / c.K[4];
+        d.z = 1.f;
+        normalize3(d.x, d.y, d.z);
+    } else {
+        const float lon = (static_cast<float>(px) - c.cx) / static_cast<float>(c.W) * 2.0f * kCudartPiF;
+        const float lat = -(static_cast<float>(py) - c.cy) / static_cast<float>(c.H) * kCudartPiF;
+        float sl, cl, sa, ca;
+        det_sincos(lon, &sl, &cl);
+        det_sincos(lat, &sa, &ca);
+        d.x = ca * sl;
+        d.y = -sa;
+        d.z = ca * cl;
+    }
+    return d;
+}
+
+__device__ __forceinline__ float3 rotate_to_world(const DevCam& c, float x, float y, float z) {
+    float3 r;
+    r.x = dot3(c.R[0], c.R[3], c.R[6], x, y, z) + c.C[0];
+    r.y = dot3(c.R[1], c.R[4], c.R[7], x, y, z) + c.C[1];
+    r.z = dot3(c.R[2], c.R[5], c.R[8], x, y, z) + c.C[2];
+    return r;
+}
+
+// Get3DPointonWorld_cu (ACMMP.cu:565-600) at arbitrary float coordinates.
+template <int MODEL>
+__device__ __forceinline__ float3 world_point(const DevCam& c, float x, float y, float depth) {
+    if (MODEL == kSphere) {
+        const float lon = (x - c.cx) / static_cast<float>(c.W) * 2.0f * kCudartPiF;
+        const float lat = -(y - c.cy) / static_cast<float>(c.H) * kCudartPiF;
+        float sl, cl, sa, ca;
+        det_sincos(lon, &sl, &cl);
+        det_sincos(lat, &sa, &ca);
+        return rotate_to_world(c, (ca * sl) * depth, (-sa) * depth, (ca * cl) * depth);
+    } else {
+        return rotate_to_world(c, (depth * (x - c.K[2])) * c.inv_fx, (depth * (y - c.K[5])) * c.inv_fy, depth);
+    }
+}
+
+// The same at an integer reference pixel whose ray `d` is already known (SPHERE's
+// camera-frame point is ray * depth exactly as Get3DPointonWorld_cu rounds it).
+template <int MODEL>
+__device__ __forceinline__ float3 world_point_ray(const DevCam& c, int x, int y, float depth, float4 d) {
+    if (MODEL == kSphere) {
+        return rotate_to_world(c, d.x * depth, d.y * depth, d.z * depth);
+    } else {
+        return rotate_to_world(c, (depth * (static_cast<float>(x) - c.K[2])) * c.inv_fx,
+                               (depth * (static_cast<float>(y) - c.K[5])) * c.inv_fy, depth);
+    }
+}
+
+// ProjectonCamera_cu, ACMMP.cu:602-644
+template <int MODEL>
+__device__ __forceinline__ void project(const DevCam& c, float3 P, float& ox, float& oy, float& depth) {
+    const float tx = dot3(c.R[0], c.R[1], c.R[2], P.x, P.y, P.z) + c.t[0];
+    const float ty = dot3(c.R[3], c.R[4], c.R[5], P.x, P.y, P.z) + c.t[1];
+    const float tz = dot3(c.R[6], c.R[7], c.R[8], P.x, P.y, P.z) + c.t[2];
+    if (MODEL == kSphere) {
+        const float d = sqrtf(dot3(tx, ty, tz, tx, ty, tz));
+        depth = d;
+        if (d < 1e-6f) { ox = c.cx; oy = c.cy; return; }
+        const float neg_lat = det_asin(ty / d);
+        const float lon = det_atan2(tx, tz);
+        ox = fmaf(lon * kInv2Pi, c.Wf, c.cx);
+        oy = fmaf(neg_lat * kInvPi, c.Hf, c.cy);
+    } else {
+        depth = tz;
+        const float inv = 1.0f / tz;
+        ox = dot3(c.K[0], c.K[1], c.K[2], tx, ty, tz) * inv;
+        oy = dot3(c.K[3], c.K[4], c.K[5], tx, ty, tz) * inv;
+    }
+}
+
+// ComputeDepthfromPlaneHypothesis, ACMMP.cu:187-193
+__device__ __forceinline__ float depth_from_plane(float4 ph, float4 d) {
+    const float denom = dot3(ph.x, ph.y, ph.z, d.x, d.y, d.z);
+    return (fabsf(denom) < 1e-6f) ? 1e6f : (-ph.w / denom);
+}
+
+// GetDistance2Origin, ACMMP.cu:168-173
+__device__ __forceinline__ float dist_to_origin(float4 d, float depth, float4 n) {
+    return -dot3(n.x, n.y, n.z, d.x * depth, d.y * depth, d.z * depth);
+}
+
+// TransformNormal / TransformNormal2RefCam, ACMMP.cu:378-396
+__device__ __forceinline__ float4 to_world(const DevCam& c, float4 n) {
+    return make_float4(dot3(c.R[0], c.R[3], c.R[6], n.x, n.y, n.z), dot3(c.R[1], c.R[4], c.R[7], n.x, n.y, n.z),
+                       dot3(c.R[2], c.R[5], c.R[8], n.x, n.y, n.z), n.w);
+}
+__device__ __forceinline__ float4 to_ref(const DevCam& c, float4 n) {
+    return make_float4(dot3(c.R[0], c.R[1], c.R[2], n.x, n.y, n.z), dot3(c.R[3], c.R[4], c.R[5], n.x, n.y, n.z),
+                       dot3(c.R[6], c.R[7], c.R[8], n.x, n.y, n.z), n.w);
+}
+
+__device__ __forceinline__ float dot3n(float4 a, float4 b) { return dot3(a.x, a.y, a.z, b.x, b.y, b.z); }
+
+// ------------------------------------------------------------------ texture fetches
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// tex2D(img, ix+0.5, iy+0.5): exact texel with clamp addressing (padded image base = texel (-1,-1))
+__device__ __forceinline__ float texel_padded(const float* img, int pitch, int W, int H, int ix, int iy) {
+    return img[static_cast<long long>(clampi(iy, 0, H - 1) + 1) * pitch + clampi(ix, 0, W - 1) + 1];
+}
+
+// tex2D(img, x+0.5, y+0.5) with fp32 bilinear weights and clamp addressing.  The one-texel
+// replicated border makes (ix, ix+1) valid for ix in [-1, W-1], which equals clamping both.
+__device__ __forceinline__ float bilinear_padded(const float* img, int pitch, int W, int H, float x, float y) {
+    const float fx = floorf(x), fy = floorf(y);
+    const float a = x - fx, b = y - fy;
+    const int ix = clampi(f2i_sat(fx), -1, W - 1);
+    const int iy = clampi(f2i_sat(fy), -1, H - 1);
+    const float* p0 = img + static_cast<long long>(iy + 1) * pitch + (ix + 1);
+    const float t00 = p0[0], t10 = p0[1], t01 = p0[pitch], t11 = p0[pitch + 1];
+    const float r0 = fmaf(a, t10 - t00, t00);
+    const float r1 = fmaf(a, t11 - t01, t01);
+    return fmaf(b, r1 - r0, r0);
+}
+
+__device__ __forceinline__ float texel_plain(const float* img, int W, int H, int ix, int iy) {
+    return img[static_cast<long long>(clampi(iy, 0, H - 1)) * W + clampi(ix, 0, W - 1)];
+}
+
+// ------------------------------------------------------------------ helpers over KParams
+
+__device__ __forceinline__ float4 ray_at(const KParams& kp, int x, int y) {
+    return kp.dirs[static_cast<long long>(y + kp.R) * kp.dpitch + (x + kp.R)];
+}
+__device__ __forceinline__ long long cs_index(const KParams& kp, int x, int y) {
+    return static_cast<long long>(y) * kp.Wh + (x >> 1);
+}
+__device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ComputeBilateralWeight, ACMMP.cu:398-403
+__device__ __forceinline__ float bilateral_weight(float dx, float dy, float pix, float center, float ss, float sc) {
+    const float sd = sqrtf(fmaf(dy, dy, dx * dx));
+    const float cd = fabsf(pix - center);
+    return det_exp((-sd) / (2.0f * ss * ss) - cd / (2.0f * sc * sc));
+}
+
+// ------------------------------------------------------------------ NCC over a chunk of views
+
+// ComputeBilateralNCC (ACMMP.cu:405-516) of plane `ph` at pixel (px, py) against the
+// source views vlist[0..nv) (wave-uniform camera indices 1..N-1), sample-outer.
+template <int MODEL, int VB>
+__device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, long long tix, long long six, float4 ph,
+                                          const int (&vlist)[VB], int nv, float (&cost)[VB]) {
+    const DevCam& rc = kp.cams[0];
+    float sbw[VB], sref[VB], srr[VB], ssrc[VB], sss[VB], srs[VB];
+    bool cval[VB];
+    const long long Pc = kp.Pc;
+    const float4 dc = ray_at(kp, px, py);
+    const float3 Pc3 = world_point_ray<MODEL>(rc, px, py, depth_from_plane(ph, dc), dc);
+    float s_bw0 = 0.f, s_ref0 = 0.f, s_rr0 = 0.f;
+    if (MODEL == kSphere) {
+        s_bw0 = kp.tsum[six];
+        s_ref0 = kp.tsum[six + Pc];
+        s_rr0 = kp.tsum[six + 2 * Pc];
+    }
+#pragma unroll
+    for (int v = 0; v < VB; ++v) {
+        sbw[v] = s_bw0; sref[v] = s_ref0; srr[v] = s_rr0;
+        ssrc[v] = 0.f; sss[v] = 0.f; srs[v] = 0.f;
+        cval[v] = true;
+        if (MODEL == kPinhole && v < nv) {
+            const DevCam& c = kp.cams[vlist[v]];
+            float ox, oy, od;
+            project<MODEL>(c, Pc3, ox, oy, od);
+            cval[v] = !(ox < 0.0f || ox >= c.Wf || oy < 0.0f || oy >= c.Hf);
+        }
+    }
+    const int R = kp.R, inc = kp.inc;
+    int s = 0;
+    for (int i = -R; i <= R; i += inc) {
+        for (int j = -R; j <= R; j += inc, ++s) {
+            const int rx = px + i, ry = py + j;
+            const float4 d = ray_at(kp, rx, ry);
+            const float3 P = world_point_ray<MODEL>(rc, rx, ry, depth_from_plane(ph, d), d);
+            const long long ti = tix + static_cast<long long>(s) * Pc;
+            const float w = kp.tw[ti];
+            const float wr = kp.twr[ti];
+            const float r = (MODEL == kPinhole) ? kp.tr[ti] : 0.f;
+#pragma unroll
+            for (int v = 0; v < VB; ++v) {
+                if (v < nv) {
+                    const DevCam& c = kp.cams[vlist[v]];
+                    float sx, sy, sd;
+                    project<MODEL>(c, P, sx, sy, sd);
+                    bool ok = true;
+                    if (MODEL == kSphere) {
+                        sx = fmaf(-floorf(sx * c.invW), c.Wf, sx);
+                        sy = fminf(fmaxf(sy, 0.0f), c.Hf - 1.0f);
+                    } else {
+                        ok = !(sx < 0.0f || sx >= c.Wf || sy < 0.0f || sy >= c.Hf);
+                    }
+                    if (ok) {
+                        const float sp = bilinear_padded(kp.img + c.img_off, c.img_pitch, c.W, c.H, sx, sy);
+                        if (MODEL == kPinhole) {
+                            sbw[v] += w;
+                            sref[v] = fmaf(w, r, sref[v]);
+                            srr[v] = fmaf(wr, r, srr[v]);
+                        }
+                        ssrc[v] = fmaf(w, sp, ssrc[v]);
+                        const float ws = w * sp;
+                        sss[v] = fmaf(ws, sp, sss[v]);
+                        srs[v] = fmaf(wr, sp, srs[v]);
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < VB; ++v) {
+        float out = 2.0f;
+        if (cval[v] && !(sbw[v] < 1e-6f)) {
+            const float inv = 1.0f / sbw[v];
+            const float m_ref = sref[v] * inv, m_src = ssrc[v] * inv;
+            const float e_rr = srr[v] * inv, e_ss = sss[v] * inv, e_rs = srs[v] * inv;
+            const float var_ref = fmaf(-m_ref, m_ref, e_rr);
+            const float var_src = fmaf(-m_src, m_src, e_ss);
+            if (!(var_ref < 1e-5f || var_src < 1e-5f)) {
+                const float covar = fmaf(-m_ref, m_src, e_rs);
+                const float ncc = 1.0f - covar / sqrtf(var_ref * var_src);
+                out = fmaxf(0.0f, fminf(2.0f, ncc));
+            }
+        }
+        cost[v] = out;
+    }
+}
+
+// ComputeGeomConsistencyCost, ACMMP.cu:646-671 (sv = source camera index 1..N-1)
+template <int MODEL>
+__device__ __forceinline__ float geom_cost(const KParams& kp, int sv, float4 ph, int px, int py, float4 dc) {
+    const DevCam& rc = kp.cams[0];
+    const DevCam& sc = kp.cams[sv];
+    const float depth = depth_from_plane(ph, dc);
+    const float3 fwd = world_point_ray<MODEL>(rc, px, py, depth, dc);
+    float sx, sy, sd;
+    project<MODEL>(sc, fwd, sx, sy, sd);
+    const float src_depth = texel_plain(kp.dep + sc.dep_off, sc.dep_w, sc.dep_h, f2i_sat(sx), f2i_sat(sy));
+    if (src_depth == 0.0f) return 3.0f;
+    const float3 s3 = world_point<MODEL>(sc, sx, sy, src_depth);
+    float bx, by, bd;
+    project<MODEL>(rc, s3, bx, by, bd);
+    const float dcol = static_cast<float>(px) - bx, drow = static_cast<float>(py) - by;
+    return fminf(3.0f, sqrtf(fmaf(drow, drow, dcol * dcol)));
+}
+
+// Views that at least one active lane of the wave needs (mask = per-lane bitmask of views 0..V-1).
+__device__ __forceinline__ uint32_t wave_or(uint32_t mask) {
+    uint32_t r = 0;
+    for (int off = 32; off >= 1; off >>= 1) mask |= __shfl_xor(mask, off);
+    r = mask;
+    return uniform_int(static_cast<int>(r));
+}
+
+// ------------------------------------------------------------------ random hypotheses
+
+// SampleDepthInv, ACMMP.cu:14-22
+__device__ __forceinline__ float sample_depth_inv(Rng& rs, float dmin, float dmax) {
+    dmin = fmaxf(dmin, 1e-6f);
+    dmax = fmaxf(dmax, dmin + 1e-6f);
+    const float inv_min = 1.0f / dmax;
+    const float inv_max = 1.0f / dmin;
+    const float u = rs.uniform();
+    const float inv = fmaf(u, inv_max - inv_min, inv_min);
+    return 1.0f / inv;
+}
+
+// GenerateRandomNormal, ACMMP.cu:194-220 (view ray supplied)
+__device__ __forceinline__ float4 random_normal(float4 v, Rng& rs) {
+    float q1 = 1.0f, q2 = 1.0f, s = 2.0f;
+    while (s >= 1.0f) {
+        q1 = fmaf(2.0f, rs.uniform(), -1.0f);
+        q2 = fmaf(2.0f, rs.uniform(), -1.0f);
+        s = fmaf(q2, q2, q1 * q1);
+    }
+    const float sq = sqrtf(1.0f - s);
+    float4 n = make_float4((2.0f * q1) * sq, (2.0f * q2) * sq, fmaf(-2.0f, s, 1.0f), 0.0f);
+    if (dot3n(n, v) > 0.0f) { n.x = -n.x; n.y = -n.y; n.z = -n.z; }
+    normalize3(n.x, n.y, n.z);
+    return n;
+}
+
+// GeneratePerturbedNormal, ACMMP.cu:222-257
+__device__ __forceinline__ float4 perturbed_normal(float4 v, float4 n, Rng& rs, float perturbation) {
+    const float a1 = (rs.uniform() - 0.5f) * perturbation;
+    const float a2 = (rs.uniform() - 0.5f) * perturbation;
+    const float a3 = (rs.uniform() - 0.5f) * perturbation;
+    float s1, c1, s2, c2, s3, c3;
+    det_sincos(a1, &s1, &c1);
+    det_sincos(a2, &s2, &c2);
+    det_sincos(a3, &s3, &c3);
+    const float R0 = c2 * c3;
+    const float R1 = fmaf(-c1, s3, (c3 * s1) * s2);
+    const float R2 = fmaf(c1 * c3, s2, s1 * s3);
+    const float R3 = c2 * s3;
+    const float R4 = fmaf(s1 * s2, s3, c1 * c3);
+    const float R5 = fmaf(-c3, s1, (c1 * s2) * s3);
+    const float R6 = -s2;
+    const float R7 = c2 * s1;
+    const float R8 = c1 * c2;
+    float4 p = make_float4(dot3(R0, R1, R2, n.x, n.y, n.z), dot3(R3, R4, R5, n.x, n.y, n.z),
+                           dot3(R6, R7, R8, n.x, n.y, n.z), n.w);
+    if (dot3n(p, v) >= 0.0f) p = n;
+    normalize3(p.x, p.y, p.z);
+    return p;
+}
+
+// ------------------------------------------------------------------ cost-vector helpers
+
+// Evaluate all source views of plane `ph` and hand each cost to f(view0, cost) in view order.
+template <int MODEL, int VB, typename F>
+__device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py, long long tix, long long six,
+                                              float4 ph, uint32_t wave_mask, F&& f) {
+    int v = 0;
+    const int V = kp.V;
+    while (true) {
+        int vlist[VB];
+        int nv = 0;
+        // next VB views present in wave_mask (wave-uniform)
+#pragma unroll
+        for (int k = 0; k < VB; ++k) vlist[k] = 1;
+        while (v < V && nv < VB) {
+            if ((wave_mask >> v) & 1u) {
+#pragma unroll
+                for (int k = 0; k < VB; ++k)
+                    if (k == nv) vlist[k] = v + 1;
+                ++nv;
+            }
+            ++v;
+        }
+        if (nv == 0) break;
+        float cost[VB];
+        ncc_chunk<MODEL, VB>(kp, px, py, tix, six, ph, vlist, nv, cost);
+#pragma unroll
+        for (int k = 0; k < VB; ++k)
+            if (k < nv) f(vlist[k] - 1, cost[k]);
+        if (v >= V) break;
+    }
+}
+
+__device__ __forceinline__ float vw_get(const uint32_t (&vwp)[4], int v) {
+    const uint32_t word = v < 8 ? vwp[0] : (v < 16 ? vwp[1] : (v < 24 ? vwp[2] : vwp[3]));
+    return static_cast<float>((word >> ((v & 7) * 4)) & 15u);
+}
+
+// ------------------------------------------------------------------ kernels: setup
+
+__global__ void k_pad_image(const float* __restrict__ src, size_t pitch, int W, int H, float* __restrict__ dst,
+                            int dpitch) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x - 1;
+    const int y = blockIdx.y * blockDim.y + threadIdx.y - 1;
+    if (x > W || y > H) return;
+    dst[static_cast<long long>(y + 1) * dpitch + (x + 1)] =
+        src[static_cast<long long>(clampi(y, 0, H - 1)) * pitch + clampi(x, 0, W - 1)];
+}
+
+__global__ void k_dir_table(const KParams kp, float4* __restrict__ dirs) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y * blockDim.y + threadIdx.y;
+    const int TW = kp.W + 2 * kp.R, TH = kp.H + 2 * kp.R;
+    if (x >= TW || y >= TH) return;
+    const float3 d = pixel_to_dir(kp.cams[0], x - kp.R, y - kp.R);
+    dirs[static_cast<long long>(y) * kp.dpitch + x] = make_float4(d.x, d.y, d.z, 0.0f);
+}
+
+// Per-pixel patch tables (colour-split): w, w*ref, ref for each of the S samples, plus the
+// hypothesis-independent SPHERE sums.  ACMMP.cu:436-493.
+template <int MODEL>
+__global__ void k_prepare(const KParams kp, float* __restrict__ tw, float* __restrict__ twr, float* __restrict__ tr,
+                          float* __restrict__ tsum) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y * blockDim.y + threadIdx.y;
+    const int colour = blockIdx.z;
+    const int x = 2 * k + ((y + colour) & 1);
+    if (x >= kp.W || y >= kp.H) return;
+    const DevCam& rc = kp.cams[0];
+    const long long Pc = kp.Pc;
+    const long long tix = static_cast<long long>(colour) * kp.S * Pc + static_cast<long long>(y) * kp.Wh + k;
+    const float* ref = kp.img + rc.img_off;
+    float scale_x = 1.0f, scale_y = 1.0f, sig = kp.sigma_spatial;
+    if (MODEL == kSphere) {
+        const float lat_c = -(static_cast<float>(y) - rc.cy) / static_cast<float>(rc.H) * kCudartPiF;
+        scale_x = (2.0f * kCudartPiF / static_cast<float>(rc.W)) * det_cos(lat_c);
+        scale_y = (kCudartPiF / static_cast<float>(rc.H));
+        sig = kp.sigma_spatial * (kCudartPiF / static_cast<float>(rc.H));
+    }
+    const float center = texel_padded(ref, rc.img_pitch, rc.W, rc.H, x, y);
+    float sbw = 0.f, sref = 0.f, srr = 0.f;
+    int s = 0;
+    for (int i = -kp.R; i <= kp.R; i += kp.inc) {
+        for (int j = -kp.R; j <= kp.R; j += kp.inc, ++s) {
+            const float r = texel_padded(ref, rc.img_pitch, rc.W, rc.H, x + i, y + j);
+            const float dx = MODEL == kSphere ? static_cast<float>(i) * scale_x : static_cast<float>(i);
+            const float dy = MODEL == kSphere ? static_cast<float>(j) * scale_y : static_cast<float>(j);
+            const float w = bilateral_weight(dx, dy, r, center, sig, kp.sigma_color);
+            const float wr = w * r;
+            tw[tix + s * Pc] = w;
+            twr[tix + s * Pc] = wr;
+            tr[tix + s * Pc] = r;
+            sbw += w;
+            sref = fmaf(w, r, sref);
+            srr = fmaf(wr, r, srr);
+        }
+    }
+    const long long si = static_cast<long long>(colour) * 3 * Pc + static_cast<long long>(y) * kp.Wh + k;
+    tsum[si] = sbw;
+    tsum[si + Pc] = sref;
+    tsum[si + 2 * Pc] = srr;
+}
+
+// ------------------------------------------------------------------ initial cost
+
+__device__ __forceinline__ void sort_small(float* d, int n) {
+    int j;
+    for (int i = 1; i < n; i++) {
+        const float tmp = d[i];
+        for (j = i; j >= 1 && tmp < d[j - 1]; j--) d[j] = d[j - 1];
+        d[j] = tmp;
+    }
+}
+
+// ComputeMultiViewInitialCostandSelectedViews, ACMMP.cu:519-556
+template <int MODEL, int VB>
+__device__ float initial_cost(const KParams& kp, int px, int py, long long tix, long long six, float4 ph,
+                             uint32_t* sel) {
+    float cv[kMaxViews], cvc[kMaxViews];
+    int nvalid = 0;
+    const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
+    for_all_views<MODEL, VB>(kp, px, py, tix, six, ph, all, [&](int v, float c) {
+        cv[v] = c;
+        cvc[v] = c;
+        if (c < 2.0f) nvalid++;
+    });
+    sort_small(cv, kp.V);
+    *sel = 0;
+    const int top_k = nvalid < kp.top_k ? nvalid : kp.top_k;
+    if (top_k > 0) {
+        float cost = 0.0f;
+        for (int i = 0; i < top_k; ++i) cost += cv[i];
+        const float thr = cv[top_k - 1];
+        for (int i = 0; i < kp.V; ++i)
+            if (cvc[i] <= thr) *sel |= (1u << i);
+        return cost / static_cast<float>(top_k);
+    }
+    return 2.0f;
+}
+
+// SpatialGauss / RangeGauss, ACMMP.cu:175-185 (float exponent)
+__device__ __forceinline__ float spatial_gauss(float x1, float y1, float x2, float y2, float sigma) {
+    const float dx = x1 - x2, dy = y1 - y2;
+    const float dis = (dx * dx + dy * dy) - 0.0f;
+    return det_exp(-dis / (2.0f * sigma * sigma));
+}
+__device__ __forceinline__ float range_gauss(float x, float sigma) {
+    const float xp = x - 0.0f;
+    return det_exp(-(xp * xp) / (2.0f * sigma * sigma));
+}
+
+// ------------------------------------------------------------------ kernel: RandomInitialization
+
+// ACMMP.cu:673-795.  Reads the persistent row-major state, writes the colour-split working state.
+template <int MODEL, int VB>
+__global__ __launch_bounds__(256) void k_init(const KParams kp) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y * blockDim.y + threadIdx.y;
+    if (x >= kp.W || y >= kp.H) return;
+    const DevCam& rc = kp.cams[0];
+    const long long center = static_cast<long long>(y) * kp.W + x;
+    const int colour = (x + y) & 1;
+    const long long ci = cs_index(kp, x, y);
+    const long long tix = static_cast<long long>(colour) * kp.S * kp.Pc + ci;
+    const long long six = static_cast<long long>(colour) * 3 * kp.Pc + ci;
+    Rng rs;
+    rs.init(kp.seed_lo, kp.seed_hi, static_cast<uint32_t>(center), 0u);
+    const float4 dc = ray_at(kp, x, y);
+    float4 ph;
+    float cost;
+    uint32_t sel = 0;
+    if (!kp.geom && !kp.hier) {
+        const float depth = fmaf(rs.uniform(), kp.depth_max - kp.depth_min, kp.depth_min);
+        ph = random_normal(dc, rs);
+        ph.w = dist_to_origin(dc, depth, ph);
+        cost = initial_cost<MODEL, VB>(kp, x, y, tix, six, ph, &sel);
+    } else if (kp.planar) {
+        if (kp.mask[center] > 0 && kp.costs_rm[center] >= 0.1f) {
+            const float perturbation = 0.02f;
+            const float4 prior = kp.prior[center];
+            float dp = prior.w;
+            const float dmin_p = (1 - 3 * perturbation) * dp;
+            const float dmax_p = (1 + 3 * perturbation) * dp;
+            dp = fmaf(rs.uniform(), dmax_p - dmin_p, dmin_p);
+            ph = perturbed_normal(dc, prior, rs, static_cast<float>(3 * perturbation * kMPi));
+            ph.w = dp;
+        } else {
+            ph = kp.planes_rm[center];
+            const float depth = ph.w;
+            ph.w = dist_to_origin(dc, depth, ph);
+        }
+        cost = initial_cost<MODEL, VB>(kp, x, y, tix, six, ph, &sel);
+    } else if (kp.upsample) {
+        const float scale = static_cast<float>(1.0 * static_cast<double>(kp.scaled_cols) / static_cast<double>(kp.W));
+        const float sigmad = 0.50f, sigmar = 25.5f;
+        const int Imagescale = f2i_sat(fmaxf(static_cast<float>(kp.W) / kp.scaled_cols,
+                                             static_cast<float>(kp.H) / kp.scaled_rows));
+        const int nn = (Imagescale * Imagescale + 1) / 2;
+        const float o_y = static_cast<float>(y) * scale, o_x = static_cast<float>(x) * scale;
+        const float* ref = kp.img + rc.img_off;
+        const float refPix = texel_padded(ref, rc.img_pitch, rc.W, rc.H, x, y);
+        float nf = 0.0f;
+        float nx = 0.f, ny = 0.f, nz = 0.f;
+        for (int j = -nn; j <= nn; ++j) {
+            int r_y = f2i_sat(o_y + static_cast<float>(j));
+            r_y = (r_y > 0 ? (static_cast<float>(r_y) < kp.scaled_rows ? r_y : f2i_sat(kp.scaled_rows - 1)) : 0);
+            const int r_ys = y + j;
+            for (int i = -nn; i <= nn; ++i) {
+                int r_x = f2i_sat(o_x + static_cast<float>(i));
+                r_x = (r_x > 0 ? (static_cast<float>(r_x) < kp.scaled_cols ? r_x : f2i_sat(kp.scaled_cols - 1)) : 0);
+                const int s_center = f2i_sat(static_cast<float>(r_y) * kp.scaled_cols + static_cast<float>(r_x));
+                const float4 sn = kp.scaled[s_center];
+                const float nbPix = texel_padded(ref, rc.img_pitch, rc.W, rc.H, x + i, r_ys);
+                const float tg = spatial_gauss(o_x, o_y, static_cast<float>(r_x), static_cast<float>(r_y), sigmad) *
+                                 range_gauss(fabsf(refPix - nbPix), sigmar);
+                nf += tg;
+                nx = nx + sn.x * tg;
+                ny = ny + sn.y * tg;
+                nz = nz + sn.z * tg;
+            }
+        }
+        nx = nx / nf; ny = ny / nf; nz = nz / nf;
+        normalize3(nx, ny, nz);
+        const float4 cur = kp.planes_rm[center];
+        uint32_t sel0;
+        kp.pre_rm[center] = initial_cost<MODEL, VB>(kp, x, y, tix, six, cur, &sel0);
+        ph = to_ref(rc, make_float4(nx, ny, nz, 0.0f));
+        ph.w = dist_to_origin(dc, cur.w, ph);
+        cost = initial_cost<MODEL, VB>(kp, x, y, tix, six, ph, &sel);
+    } else {
+        ph = kp.hier ? kp.scaled[center] : kp.planes_rm[center];
+        ph = to_ref(rc, ph);
+        const float depth = ph.w;
+        ph.w = dist_to_origin(dc, depth, ph);
+        cost = initial_cost<MODEL, VB>(kp, x, y, tix, six, ph, &sel);
+    }
+    kp.plane_cs[colour][ci] = ph;
+    kp.cost_cs[colour][ci] = cost;
+    kp.sel_cs[colour][ci] = sel;
+    kp.rng_cs[colour][ci] = rs.n;
+}
+
+// ------------------------------------------------------------------ kernel: CheckerboardPropagation
+
+__device__ __forceinline__ float cost_at(const KParams& kp, int x, int y) {
+    return kp.cost_cs[(x + y) & 1][cs_index(kp, x, y)];
+}
+__device__ __forceinline__ float4 plane_at(const KParams& kp, int pos) {
+    const int x = pos & 0xFFFF, y = pos >> 16;
+    return kp.plane_cs[(x + y) & 1][cs_index(kp, x, y)];
+}
+__device__ __forceinline__ int packpos(int x, int y) { return x | (y << 16); }
+
+// ACMMP.cu:938-1325 + 1327-1349 for one colour; snapshot semantics.
+template <int MODEL, int VB>
+__global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int colour, const int iter,
+                                                   const SweepOut out) {
+    const int kx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int py = blockIdx.y * blockDim.y + threadIdx.y;
+    const int px = 2 * kx + ((py + colour) & 1);
+    if (py >= kp.rows || px >= kp.W) return;
+    const int width = kp.W, height = kp.H, V = kp.V;
+    const long long Pc = kp.Pc;
+    const long long ci = static_cast<long long>(py) * kp.Wh + kx;
+    const long long tix = static_cast<long long>(colour) * kp.S * Pc + ci;
+    const long long six = static_cast<long long>(colour) * 3 * Pc + ci;
+    const long long center = static_cast<long long>(py) * width + px;
+    const float4 dc = ray_at(kp, px, py);
+    Rng rs;
+    rs.init(kp.seed_lo, kp.seed_hi, static_cast<uint32_t>(center), kp.rng_cs[colour][ci]);
+
+    // ---- adaptive checkerboard sampling :965-1143 (positions packed x | y << 16)
+    int pos[8];
+    bool flag[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) { flag[d] = false; pos[d] = 0; }
+    {
+        float cmin; int cpos;
+        if (py > 2) {                                           // up_far
+            flag[1] = true; cmin = cost_at(kp, px, py - 3); cpos = packpos(px, py - 3);
+            for (int i = 1; i < 11; ++i) if (py > 2 + 2 * i) {
+                const float c = cost_at(kp, px, py - 3 - 2 * i);
+                if (c < cmin) { cmin = c; cpos = packpos(px, py - 3 - 2 * i); }
+            }
+            pos[1] = cpos;
+        }
+        if (py < height - 3) {                                  // down_far
+            flag[3] = true; cmin = cost_at(kp, px, py + 3); cpos = packpos(px, py + 3);
+            for (int i = 1; i < 11; ++i) if (py < height - 3 - 2 * i) {
+                const float c = cost_at(kp, px, py + 3 + 2 * i);
+                if (c < cmin) { cmin = c; cpos = packpos(px, py + 3 + 2 * i); }
+            }
+            pos[3] = cpos;
+        }
+        if (px > 2) {                                           // left_far
+            flag[5] = true; cmin = cost_at(kp, px - 3, py); cpos = packpos(px - 3, py);
+            for (int i = 1; i < 11; ++i) if (px > 2 + 2 * i) {
+                const float c = cost_at(kp, px - 3 - 2 * i, py);
+                if (c < cmin) { cmin = c; cpos = packpos(px - 3 - 2 * i, py); }
+            }
+            pos[5] = cpos;
+        }
+        if (px < width - 3) {                                   // right_far
+            flag[7] = true; cmin = cost_at(kp, px + 3, py); cpos = packpos(px + 3, py);
+            for (int i = 1; i < 11; ++i) if (px < width - 3 - 2 * i) {
+                const float c = cost_at(kp, px + 3 + 2 * i, py);
+                if (c < cmin) { cmin = c; cpos = packpos(px + 3 + 2 * i, py); }
+            }
+            pos[7] = cpos;
+        }
+        if (py > 0) {                                           // up_near (V shape, same colour)
+            flag[0] = true; cmin = cost_at(kp, px, py - 1); cpos = packpos(px, py - 1);
+            for (int i = 0; i < 3; ++i) {
+                if (py > 1 + i && px > i) {
+                    const float c = cost_at(kp, px - i, py - 2 - i);
+                    if (c < cmin) { cmin = c; cpos = packpos(px - i, py - 2 - i); }
+                }
+                if (py > 1 + i && px < width - 1 - i) {
+                    const float c = cost_at(kp, px + i, py - 2 - i);
+                    if (c < cmin) { cmin = c; cpos = packpos(px + i, py - 2 - i); }
+                }
+            }
+            pos[0] = cpos;
+        }
+        if (py < height - 1) {                                  // down_near
+            flag[2] = true; cmin = cost_at(kp, px, py + 1); cpos = packpos(px, py + 1);
+            for (int i = 0; i < 3; ++i) {
+                if (py < height - 2 - i && px > i) {
+                    const float c = cost_at(kp, px - i, py + 2 + i);
+                    if (c < cmin) { cmin = c; cpos = packpos(px - i, py + 2 + i); }
+                }
+                if (py < height - 2 - i && px < width - 1 - i) {
+                    const float c = cost_at(kp, px + i, py + 2 + i);
+                    if (c < cmin) { cmin = c; cpos = packpos(px + i, py + 2 + i); }
+                }
+            }
+            pos[2] = cpos;
+        }
+        if (px > 0) {                                           // left_near
+            flag[4] = true; cmin = cost_at(kp, px - 1, py); cpos = packpos(px - 1, py);
+            for (int i = 0; i < 3; ++i) {
+                if (px > 1 + i && py > i) {
+                    const float c = cost_at(kp, px - 2 - i, py - i);
+                    if (c < cmin) { cmin = c; cpos = packpos(px - 2 - i, py - i); }
+                }
+                if (px > 1 + i && py < height - 1 - i) {
+                    const float c = cost_at(kp, px - 2 - i, py + i);
+                    if (c < cmin) { cmin = c; cpos = packpos(px - 2 - i, py + i); }
+                }
+            }
+            pos[4] = cpos;
+        }
+        if (px < width - 1) {                                   // right_near
+            flag[6] = true; cmin = cost_at(kp, px + 1, py); cpos = packpos(px + 1, py);
+            for (int i = 0; i < 3; ++i) {
+                if (px < width - 2 - i && py > i) {
+                    const float c = cost_at(kp, px + 2 + i, py - i);
+                    if (c < cmin) { cmin = c; cpos = packpos(px + 2 + i, py - i); }
+                }
+                if (px < width - 2 - i && py < height - 1 - i) {
+                    const float c = cost_at(kp, px + 2 + i, py + i);
+                    if (c < cmin) { cmin = c; cpos = packpos(px + 2 + i, py + i); }
+                }
+            }
+            pos[6] = cpos;
+        }
+    }
+
+    // ---- 8 x V cost matrix into the scratch slab [d][v][Pc]
+    const uint32_t all = V >= 32 ? 0xFFFFFFFFu : ((1u << V) - 1u);
+    float* scr = kp.scratch;
+    for (int d = 0; d < 8; ++d) {
+        float4 nb = make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool f = flag[d];
+        if (f) nb = plane_at(kp, pos[d]);
+        if (f) {
+            for_all_views<MODEL, VB>(kp, px, py, tix, six, nb, all, [&](int v, float c) {
+                scr[(static_cast<long long>(d) * V + v) * Pc + ci] = c;
+            });
+        } else {
+            for (int v = 0; v < V; ++v)
+                scr[(static_cast<long long>(d) * V + v) * Pc + ci] = (d == 0 && v == 0) ? 2.0f : 0.0f;
+        }
+    }
+    auto cost_arr = [&](int d, int v) -> float { return scr[(static_cast<long long>(d) * V + v) * Pc + ci]; };
+
+    // ---- joint view selection :1146-1208
+    float vsp[kMaxViews];
+    for (int j = 0; j < V; ++j) vsp[j] = 0.0f;
+    {
+        const int nbx[4] = {px, px, px - 1, px + 1};
+        const int nby[4] = {py - 1, py + 1, py, py};
+        for (int i = 0; i < 4; ++i) {
+            if (flag[2 * i]) {
+                const uint32_t sv = kp.sel_cs[(nbx[i] + nby[i]) & 1][cs_index(kp, nbx[i], nby[i])];
+                for (int j = 0; j < V; ++j) vsp[j] += ((sv >> j) & 1u) ? 0.9f : 0.1f;
+            }
+        }
+    }
+    const float cost_threshold = static_cast<float>(0.8 * static_cast<double>(
+        det_exp(static_cast<float>(iter * iter) / (-90.0f))));
+    float probs[kMaxViews];
+    for (int i = 0; i < V; i++) {
+        float count = 0.0f;
+        int count_false = 0;
+        float tmpw = 0.0f;
+        for (int j = 0; j < 8; j++) {
+            const float c = cost_arr(j, i);
+            if (c < cost_threshold) { tmpw += det_exp(c * c / (-0.18f)); count++; }
+            if (c > 1.2f) count_false++;
+        }
+        float pr = 0.0f;
+        if (count > 2 && count_false < 3) pr = tmpw / count;
+        else if (count_false < 3) pr = det_exp(cost_threshold * cost_threshold / (-0.32f));
+        probs[i] = pr * vsp[i];
+    }
+    {
+        float prob_sum = 0.0f;
+        for (int i = 0; i < V; ++i) prob_sum += probs[i];
+        const float inv = 1.0f / prob_sum;
+        float cum = 0.0f;
+        for (int i = 0; i < V; ++i) { cum = fmaf(probs[i], inv, cum); probs[i] = cum; }
+    }
+    uint32_t vwp[4] = {0u, 0u, 0u, 0u};
+    for (int sample = 0; sample < 15; ++sample) {
+        const float rp = rs.uniform() - 1.1920928955078125e-07f;
+        for (int k = 0; k < V; ++k) {
+            if (probs[k] > rp) {
+                const uint32_t inc = 1u << ((k & 7) * 4);
+                if (k < 8) vwp[0] += inc; else if (k < 16) vwp[1] += inc; else if (k < 24) vwp[2] += inc; else vwp[3] += inc;
+                break;
+            }
+        }
+    }
+    uint32_t temp_sel = 0u;
+    float weight_norm = 0.0f;
+    for (int i = 0; i < V; ++i) {
+        const float w = vw_get(vwp, i);
+        if (w > 0) { temp_sel |= (1u << i); weight_norm += w; }
+    }
+
+    // ---- aggregated costs :1210-1228
+    float final_costs[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float fc = 0.0f;
+        float4 nb = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (kp.geom && flag[i]) nb = plane_at(kp, pos[i]);
+        for (int j = 0; j < V; ++j) {
+            const float w = vw_get(vwp, j);
+            if (w > 0) {
+                if (kp.geom) {
+                    if (flag[i]) fc = fmaf(w, fmaf(0.2f, geom_cost<MODEL>(kp, j + 1, nb, px, py, dc), cost_arr(i, j)), fc);
+                    else fc = fmaf(w, cost_arr(i, j) + 0.1f * 3.0f, fc);
+                } else {
+                    fc = fmaf(w, cost_arr(i, j), fc);
+                }
+            }
+        }
+        final_costs[i] = fc / weight_norm;
+    }
+    int min_idx = 0;
+    {
+        float m = final_costs[0];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) if (final_costs[i] <= m) { m = final_costs[i]; min_idx = i; }
+    }
+
+    // ---- current hypothesis :1232-1245
+    const uint32_t wmask = wave_or(temp_sel);
+    float4 cur_plane = kp.plane_cs[colour][ci];
+    float cost_now = 0.0f;
+    for_all_views<MODEL, VB>(kp, px, py, tix, six, cur_plane, wmask, [&](int v, float c) {
+        const float w = vw_get(vwp, v);
+        if (w > 0.0f) {
+            if (kp.geom) cost_now = fmaf(w, fmaf(0.2f, geom_cost<MODEL>(kp, v + 1, cur_plane, px, py, dc), c), cost_now);
+            else cost_now = fmaf(w, c, cost_now);
+        }
+    });
+    cost_now /= weight_norm;
+    float cur_cost = cost_now;
+    uint32_t cur_sel = kp.sel_cs[colour][ci];
+    float depth_now = depth_from_plane(cur_plane, dc);
+    float restricted_cost = 0.0f;
+    const bool use_prior = kp.planar && kp.mask[center] > 0;
+
+    auto sel_plane = [&](int i) -> float4 {
+        float4 r = plane_at(kp, pos[0]);
+#pragma unroll
+        for (int k = 1; k < 8; ++k) if (k == i) r = plane_at(kp, pos[k]);
+        return r;
+    };
+    auto sel_f = [&](const float (&a)[8], int i) -> float {
+        float r = a[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) if (k == i) r = a[k];
+        return r;
+    };
+    auto sel_b = [&](const bool (&a)[8], int i) -> bool {
+        bool r = a[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) if (k == i) r = a[k];
+        return r;
+    };
+
+    if (kp.planar) {                                        // :1247-1299
+        const float gamma = 0.5f;
+        const float depth_sigma = (kp.depth_max - kp.depth_min) / 64.0f;
+        const float two_dss = 2 * depth_sigma * depth_sigma;
+        const float angle_sigma = static_cast<float>(kMPi * (5.0f / 180.0f));
+        const float two_ass = 2 * angle_sigma * angle_sigma;
+        const float4 prior = kp.prior[center];
+        const float depth_prior = depth_from_plane(prior, dc);
+        const float beta = 0.18f;
+        if (use_prior) {
+            float rfc[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                rfc[i] = 0.0f;
+                if (flag[i]) {
+                    const float4 nb = plane_at(kp, pos[i]);
+                    const float ddiff = depth_from_plane(nb, dc) - depth_prior;
+                    const float ad = det_acos(dot3n(prior, nb));
+                    const float pr = fmaf(det_exp((-ddiff) * ddiff / two_dss), det_exp((-ad) * ad / two_ass), gamma);
+                    rfc[i] = det_exp((-final_costs[i]) * final_costs[i] / beta) * pr;
+                }
+            }
+            int max_idx = 0;
+            {
+                float m = rfc[0];
+#pragma unroll
+                for (int i = 1; i < 8; ++i) if (rfc[i] >= m) { m = rfc[i]; max_idx = i; }
+            }
+            const float ddiff = depth_from_plane(cur_plane, dc) - depth_prior;
+            const float ad = det_acos(dot3n(prior, cur_plane));
+            const float pr = fmaf(det_exp((-ddiff) * ddiff / two_dss), det_exp((-ad) * ad / two_ass), gamma);
+            const float rc_now = det_exp((-cost_now) * cost_now / beta) * pr;
+            if (sel_b(flag, max_idx)) {
+                const float4 nb = sel_plane(max_idx);
+                const float db = depth_from_plane(nb, dc);
+                const float rmax = sel_f(rfc, max_idx);
+                if (db >= kp.depth_min && db <= kp.depth_max && rmax > rc_now) {
+                    depth_now = db;
+                    cur_plane = nb;
+                    cur_cost = sel_f(final_costs, max_idx);
+                    restricted_cost = rmax;
+                    cur_sel = temp_sel;
+                }
+            }
+        } else if (sel_b(flag, min_idx)) {
+            const float4 nb = sel_plane(min_idx);
+            const float db = depth_from_plane(nb, dc);
+            const float fmin = sel_f(final_costs, min_idx);
+            if (db >= kp.depth_min && db <= kp.depth_max && fmin < cost_now) {
+                depth_now = db;
+                cur_plane = nb;
+                cur_cost = fmin;
+            }
+        }
+    }
+
+    float4 plane_now = cur_plane;                           // fix A (:1301)
+    if (!kp.planar && sel_b(flag, min_idx)) {               // :1302-1311
+        const float4 nb = sel_plane(min_idx);
+        const float db = depth_from_plane(nb, dc);
+        const float fmin = sel_f(final_costs, min_idx);
+        if (db >= kp.depth_min && db <= kp.depth_max && fmin < cost_now) {
+            depth_now = db;
+            plane_now = nb;
+            cost_now = fmin;
+            cur_sel = temp_sel;
+        }
+    }
+
+    // ---- PlaneHypothesisRefinement :797-936
+    if (weight_norm > 0.0f) {
+        const float perturbation = 0.02f;
+        const float gamma = 0.5f;
+        const float depth_sigma = (kp.depth_max - kp.depth_min) / 64.0f;
+        const float two_dss = 2 * depth_sigma * depth_sigma;
+        const float angle_sigma = kCudartPiF * (5.0f / 180.0f);
+        const float two_ass = 2 * angle_sigma * angle_sigma;
+        const float beta = 0.18f;
+        float depth_rand;
+        float4 n_rand;
+        float4 prior = make_float4(0.f, 0.f, 0.f, 0.f);
+        float dprior = 0.f;
+        if (use_prior) {
+            prior = kp.prior[center];
+            dprior = depth_from_plane(prior, dc);
+            depth_rand = sample_depth_inv(rs, fmaxf(dprior - 3 * depth_sigma, kp.depth_min),
+                                          fminf(dprior + 3 * depth_sigma, kp.depth_max));
+            n_rand = perturbed_normal(dc, prior, rs, angle_sigma);
+        } else {
+            depth_rand = sample_depth_inv(rs, kp.depth_min, kp.depth_max);
+            n_rand = random_normal(dc, rs);
+        }
+        float lo = fmaxf((1.0f - perturbation) * depth_now, kp.depth_min);
+        float hi = fminf((1.0f + perturbation) * depth_now, kp.depth_max);
+        if (!(hi > lo)) { lo = kp.depth_min; hi = kp.depth_max; }
+        float depth_perturbed = depth_now;
+        bool ok = false;
+        for (int k = 0; k < 32; ++k) {
+            const float cand = sample_depth_inv(rs, lo, hi);
+            if (cand >= kp.depth_min && cand <= kp.depth_max) { depth_perturbed = cand; ok = true; break; }
+        }
+        if (!ok) depth_perturbed = fminf(fmaxf(depth_now, kp.depth_min), kp.depth_max);
+        const float4 n_pert = perturbed_normal(dc, plane_now, rs, perturbation * kCudartPiF);
+        const float d0 = depth_now;
+        const float4 p0 = plane_now;
+        for (int i = 0; i < 5; ++i) {
+            const float dep = (i == 0 || i == 2) ? depth_rand : (i == 4 ? depth_perturbed : d0);
+            float4 tp = (i == 1 || i == 2) ? n_rand : (i == 3 ? n_pert : p0);
+            tp.w = dist_to_origin(dc, dep, tp);
+            float temp_cost = 0.0f;
+            for_all_views<MODEL, VB>(kp, px, py, tix, six, tp, wmask, [&](int v, float c) {
+                const float w = vw_get(vwp, v);
+                if (w > 0.0f) {
+                    if (kp.geom) temp_cost = fmaf(w, fmaf(0.1f, geom_cost<MODEL>(kp, v + 1, tp, px, py, dc), c), temp_cost);
+                    else temp_cost = fmaf(w, c, temp_cost);
+                }
+            });
+            temp_cost /= weight_norm;
+            const float depth_before = depth_from_plane(tp, dc);
+            if (depth_before < kp.depth_min || depth_before > kp.depth_max || depth_before >= 1e6f) continue;
+            if (use_prior) {
+                const float ddiff = dep - dprior;
+                const float ac = fminf(fmaxf(dot3n(prior, tp), -1.0f), 1.0f);
+                const float ad = det_acos(ac);
+                const float pr = fmaf(det_exp((-ddiff) * ddiff / two_dss), det_exp((-ad) * ad / two_ass), gamma);
+                const float rtc = det_exp((-temp_cost) * temp_cost / beta) * pr;
+                if (rtc > restricted_cost) {
+                    depth_now = depth_before; plane_now = tp; cost_now = temp_cost; restricted_cost = rtc;
+                }
+            } else if (temp_cost < cost_now) {
+                depth_now = depth_before; plane_now = tp; cost_now = temp_cost;
+            }
+        }
+    }
+
+    if (kp.hier) {                                          // :1315-1324
+        if (cost_now < kp.pre_rm[center] - 0.1f) { cur_cost = cost_now; cur_plane = plane_now; }
+    } else {
+        cur_cost = cost_now;
+        cur_plane = plane_now;
+    }
+    out.plane[ci] = cur_plane;
+    out.cost[ci] = cur_cost;
+    kp.sel_cs[colour][ci] = cur_sel;
+    kp.rng_cs[colour][ci] = rs.n;
+}
+
+// ------------------------------------------------------------------ kernels: post
+
+// GetDepthandNormal (ACMMP.cu:1351-1364) fused with the colour-split -> row-major merge.
+__global__ void k_merge(const KParams kp, const int do_post) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y * blockDim.y + threadIdx.y;
+    if (x >= kp.W || y >= kp.H) return;
+    const int colour = (x + y) & 1;
+    const long long ci = cs_index(kp, x, y);
+    const long long center = static_cast<long long>(y) * kp.W + x;
+    float4 ph = kp.plane_cs[colour][ci];
+    if (do_post) {
+        ph.w = depth_from_plane(ph, ray_at(kp, x, y));
+        ph = to_world(kp.cams[0], ph);
+    }
+    kp.planes_rm[center] = ph;
+    kp.costs_rm[center] = kp.cost_cs[colour][ci];
+    kp.sel_rm[center] = kp.sel_cs[colour][ci];
+}
+
+// CheckerboardFilter, ACMMP.cu:1366-1480 (in place; reads only the other colour)
+__global__ void k_filter(const KParams kp, const int colour) {
+    const int kx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int py = blockIdx.y * blockDim.y + threadIdx.y;
+    const int px = 2 * kx + ((py + colour) & 1);
+    if (py >= kp.rows || px >= kp.W) return;
+    const int width = kp.W, height = kp.H;
+    const long long center = static_cast<long long>(py) * width + px;
+    if (kp.costs_rm[center] < 0.001f) return;
+    const float4* P = kp.planes_rm;
+    auto wv = [&](long long i) { return P[i].w; };
+    float filter[21];
+    int index = 0;
+    filter[index++] = wv(center);
+    const long long left = center - 1, leftleft = center - 3, up = center - width, upup = center - 3 * width;
+    const long long down = center + width, downdown = center + 3 * width, right = center + 1, rightright = center + 3;
+    if (py > 0) filter[index++] = wv(up);
+    if (py > 2) filter[index++] = wv(upup);
+    if (py > 4) filter[index++] = wv(upup - width * 2);
+    if (py < height - 1) filter[index++] = wv(down);
+    if (py < height - 3) filter[index++] = wv(downdown);
+    if (py < height - 5) filter[index++] = wv(downdown + width * 2);
+    if (px > 0) filter[index++] = wv(left);
+    if (px > 2) filter[index++] = wv(leftleft);
+    if (px > 4) filter[index++] = wv(leftleft - 2);
+    if (px < width - 1) filter[index++] = wv(right);
+    if (px < width - 3) filter[index++] = wv(rightright);
+    if (px < width - 5) filter[index++] = wv(rightright + 2);
+    if (py > 0 && px < width - 2) filter[index++] = wv(up + 2);
+    if (py < height - 1 && px < width - 2) filter[index++] = wv(down + 2);
+    if (py > 0 && px > 1) filter[index++] = wv(up - 2);
+    if (py < height - 1 && px > 1) filter[index++] = wv(down - 2);
+    if (px > 0 && py > 2) filter[index++] = wv(left - width * 2);
+    if (px < width - 1 && py > 2) filter[index++] = wv(right - width * 2);
+    if (px > 0 && py < height - 2) filter[index++] = wv(left + width * 2);
+    if (px < width - 1 && py < height - 2) filter[index++] = wv(right + width * 2);
+    sort_small(filter, index);
+    const int mi = index / 2;
+    const float med = (index % 2 == 0) ? (filter[mi - 1] + filter[mi]) / 2 : filter[mi];
+    kp.planes_rm[center].w = med;
+}
+
+// JBU_cu, ACMMP.cu:1558-1616
+__global__ void k_jbu(const float* __restrict__ ref, int W, int H, const float* __restrict__ coarse, int sw, int sh,
+                      int imagescale, float* __restrict__ out) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y * blockDim.y + threadIdx.y;
+    if (x >= W || y >= H) return;
+    const float scale = static_cast<float>(1.0 * static_cast<double>(sw) / static_cast<double>(W));
+    const float sigmad = 0.50f, sigmar = 25.5f;
+    const int nn = (imagescale * imagescale + 1) / 2;
+    const float o_y = static_cast<float>(y) * scale, o_x = static_cast<float>(x) * scale;
+    const float refPix = texel_plain(ref, W, H, x, y);
+    float total = 0.0f, nf = 0.0f;
+    for (int j = -nn; j <= nn; ++j) {
+        int r_y = f2i_sat(o_y + static_cast<float>(j));
+        r_y = (r_y > 0 ? (r_y < sh ? r_y : sh - 1) : 0);
+        int r_ys = y + j;
+        r_ys = (r_ys > 0 ? (r_ys < H ? r_ys : H - 1) : 0);
+        for (int i = -nn; i <= nn; ++i) {
+            int r_x = f2i_sat(o_x + static_cast<float>(i));
+            r_x = (r_x > 0 ? (r_x < sw ? r_x : sw - 1) : 0);
+            const float srcPix = texel_plain(coarse, sw, sh, r_x, r_y);
+            int r_xs = x + i;
+            r_xs = (r_xs > 0 ? (r_xs < W ? r_xs : W - 1) : 0);
+            const float nbPix = texel_plain(ref, W, H, r_xs, r_ys);
+            const float tg = spatial_gauss(o_x, o_y, static_cast<float>(r_x), static_cast<float>(r_y), sigmad) *
+                             range_gauss(fabsf(refPix - nbPix), sigmar);
+            nf += tg;
+            total = fmaf(srcPix, tg, total);
+        }
+    }
+    out[static_cast<long long>(y) * W + x] = total / nf;
+}
+
+// Test hooks: NCC / geom cost of arbitrary (pixel, plane) queries against every source view.
+template <int MODEL, int VB>
+__global__ void k_debug(const KParams kp, int which, int n, const int* __restrict__ qx, const int* __restrict__ qy,
+                        const float4* __restrict__ planes, float* __restrict__ out) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const int x = qx[q], y = qy[q];
+    const float4 ph = planes[q];
+    const int colour = (x + y) & 1;
+    const long long tix = static_cast<long long>(colour) * kp.S * kp.Pc + cs_index(kp, x, y);
+    const long long six = static_cast<long long>(colour) * 3 * kp.Pc + cs_index(kp, x, y);
+    const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
+    if (which == 0) {
+        for_all_views<MODEL, VB>(kp, x, y, tix, six, ph, all,
+                                 [&](int v, float c) { out[static_cast<long long>(q) * kp.V + v] = c; });
+    } else {
+        const float4 dc = ray_at(kp, x, y);
+        for (int v = 0; v < kp.V; ++v)
+            out[static_cast<long long>(q) * kp.V + v] = geom_cost<MODEL>(kp, v + 1, ph, x, y, dc);
+    }
+}
+
+// ------------------------------------------------------------------ host launchers
+
+static inline int cdiv(long long a, int b) { return static_cast<int>((a + b - 1) / b); }
+
+hipError_t launch_pad_image(const float* src, size_t pitch_floats, int W, int H, float* dst, int dst_pitch,
+                            hipStream_t s) {
+    dim3 blk(64, 4), grd(cdiv(W + 2, 64), cdiv(H + 2, 4));
+    k_pad_image<<<grd, blk, 0, s>>>(src, pitch_floats, W, H, dst, dst_pitch);
+    return hipGetLastError();
+}
+
+hipError_t launch_dir_table(const KParams& kp, float4* dirs, hipStream_t s) {
+    dim3 blk(64, 4), grd(cdiv(kp.W + 2 * kp.R, 64), cdiv(kp.H + 2 * kp.R, 4));
+    k_dir_table<<<grd, blk, 0, s>>>(kp, dirs);
+    return hipGetLastError();
+}
+
+hipError_t launch_prepare(const KParams& kp, hipStream_t s) {
+    dim3 blk(64, 4), grd(cdiv(kp.Wh, 64), cdiv(kp.H, 4), 2);
+    float* tw = const_cast<float*>(kp.tw);
+    float* twr = const_cast<float*>(kp.twr);
+    float* tr = const_cast<float*>(kp.tr);
+    float* ts = const_cast<float*>(kp.tsum);
+    if (kp.model == kSphere) k_prepare<kSphere><<<grd, blk, 0, s>>>(kp, tw, twr, tr, ts);
+    else k_prepare<kPinhole><<<grd, blk, 0, s>>>(kp, tw, twr, tr, ts);
+    return hipGetLastError();
+}
+
+// View-chunk width: the per-view accumulators live in registers (6 per view).
+static inline int pick_vb(int V) { return V <= 1 ? 1 : (V <= 2 ? 2 : (V <= 4 ? 4 : 8)); }
+
+#define ACMMP_DISPATCH(MODEL_RT, V_RT, BODY)                                             \
+    do {                                                                                \
+        const int vb_ = pick_vb(V_RT);                                                  \
+        if ((MODEL_RT) == kSphere) {                                                    \
+            constexpr int M = kSphere;                                                  \
+            if (vb_ == 1) { constexpr int VBC = 1; BODY; }                              \
+            else if (vb_ == 2) { constexpr int VBC = 2; BODY; }                         \
+            else if (vb_ == 4) { constexpr int VBC = 4; BODY; }                         \
+            else { constexpr int VBC = 8; BODY; }                                       \
+        } else {                                                                        \
+            constexpr int M = kPinhole;                                                 \
+            if (vb_ == 1) { constexpr int VBC = 1; BODY; }                              \
+            else if (vb_ == 2) { constexpr int VBC = 2; BODY; }                         \
+            else if (vb_ == 4) { constexpr int VBC = 4; BODY; }                         \
+            else { constexpr int VBC = 8; BODY; }                                       \
+        }                                                                               \
+    } while (0)
+
+hipError_t launch_init(const KParams& kp, hipStream_t s) {
+    dim3 blk(16, 16), grd(cdiv(kp.W, 16), cdiv(kp.H, 16));
+    ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC><<<grd, blk, 0, s>>>(kp)));
+    return hipGetLastError();
+}
+
+hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s) {
+    dim3 blk(64, 4), grd(cdiv(kp.Wh, 64), cdiv(kp.rows, 4));
+    ACMMP_DISPATCH(kp.model, kp.V, (k_propagate<M, VBC><<<grd, blk, 0, s>>>(kp, colour, iter, out)));
+    return hipGetLastError();
+}
+
+hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s) {
+    {
+        dim3 blk(64, 4), grd(cdiv(kp.W, 64), cdiv(kp.H, 4));
+        k_merge<<<grd, blk, 0, s>>>(kp, do_post);
+    }
+    if (do_post) {
+        dim3 blk(64, 4), grd(cdiv(kp.Wh, 64), cdiv(kp.rows, 4));
+        k_filter<<<grd, blk, 0, s>>>(kp, 0);
+        k_filter<<<grd, blk, 0, s>>>(kp, 1);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int sw, int sh, int imagescale,
+                      float* out, hipStream_t s) {
+    dim3 blk(16, 16), grd(cdiv(W, 16), cdiv(H, 16));
+    k_jbu<<<grd, blk, 0, s>>>(ref, W, H, coarse, sw, sh, imagescale, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,
+                        float* out, hipStream_t s) {
+    dim3 blk(64), grd(cdiv(n, 64));
+    ACMMP_DISPATCH(kp.model, kp.V, (k_debug<M, VBC><<<grd, blk, 0, s>>>(kp, which, n, px, py, planes, out)));
+    return hipGetLastError();
+}
+
+}  // namespace acmmp

@@ -1,0 +1,161 @@
+/*
+ * acmmp.h -- C ABI of the MI355X-native ACMMP-Spherical PatchMatch engine.
+ *
+ * Drop-in boundary for the depth/normal inference path of the reference
+ * (/root/reference, contineu-ai/ACMMP-Spherical @ 2025-11-21).  The reference's only
+ * caller of the hot path is ProcessProblem (main.cpp:73-210), which drives the
+ * ACMMP class (ACMMP.h:57-111).  Every entry point below names the reference
+ * member it replaces.  Plain C types only: pointers and sizes, no torch/HIP types.
+ *
+ * Threading: one context = one GPU = one host thread at a time (the reference is
+ * single-threaded and not re-entrant either).  All host pointers are borrowed for
+ * the duration of the call.  Errors are returned as acmmp_status codes; the C++
+ * facade (acmmp-spherical_amd/host/ACMMP.h) maps them to the reference's
+ * print-and-exit behaviour of CUDA_SAFE_CALL (ACMMP.cpp:64-72).
+ */
+#ifndef ACMMP_C_ABI_H
+#define ACMMP_C_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACMMP_ABI_VERSION 1
+
+/* CameraModel, main.h:184-187 */
+#define ACMMP_PINHOLE 0
+#define ACMMP_SPHERE 11
+
+/* Camera, main.h:189-203 -- identical layout (120 bytes). */
+typedef struct acmmp_camera {
+    int32_t model;          /* ACMMP_PINHOLE or ACMMP_SPHERE */
+    float params[4];        /* SPHERE: f, cx, cy, unused */
+    float R[9];             /* world -> camera rotation, row-major */
+    float t[3];             /* X_cam = R X_world + t */
+    float K[9];             /* PINHOLE intrinsics, row-major */
+    int32_t width, height;
+    float depth_min, depth_max;
+} acmmp_camera;
+
+/* PatchMatchParams, ACMMP.h:32-55 -- identical layout (68 bytes). */
+typedef struct acmmp_params {
+    int32_t max_iterations;     /* 3; SetGeomConsistencyParams sets 2 (ACMMP.cpp:551) */
+    int32_t patch_size;         /* 11 */
+    int32_t num_images;         /* reference + sources, 2..33 */
+    int32_t max_image_size;     /* 3200 */
+    int32_t radius_increment;   /* 2 */
+    float sigma_spatial;        /* 5 */
+    float sigma_color;          /* 3 */
+    int32_t top_k;              /* 4 */
+    float baseline;             /* 0.54 (unused by the hot path) */
+    float depth_min;            /* cams[0].depth_min * 0.6 (ACMMP.cpp:645) */
+    float depth_max;            /* cams[0].depth_max * 1.2 (ACMMP.cpp:646) */
+    float disparity_min;        /* unused by the hot path */
+    float disparity_max;
+    float scaled_cols;          /* hierarchy: coarse map size (ACMMP.cpp:810-811) */
+    float scaled_rows;
+    uint8_t geom_consistency;
+    uint8_t planar_prior;
+    uint8_t multi_geometry;
+    uint8_t hierarchy;
+    uint8_t upsample;
+    uint8_t _pad[3];
+} acmmp_params;
+
+typedef enum acmmp_status {
+    ACMMP_OK = 0,
+    ACMMP_ERR_INVALID_ARGUMENT = 1,
+    ACMMP_ERR_HIP = 2,
+    ACMMP_ERR_OUT_OF_MEMORY = 3,
+    ACMMP_ERR_STATE = 4,            /* call order violated (e.g. run before upload) */
+    ACMMP_ERR_UNSUPPORTED = 5,      /* e.g. mixed camera models, > 32 source views */
+    ACMMP_ERR_NO_DEVICE = 6
+} acmmp_status;
+
+typedef struct acmmp_ctx acmmp_ctx;
+
+/* ACMMP::ACMMP() (ACMMP.cpp:99) + cudaSetDevice (main.cpp:77).  `device` is a HIP
+ * ordinal; -1 keeps the calling thread's current device. */
+acmmp_status acmmp_create(int device, acmmp_ctx **out);
+/* ACMMP::~ACMMP() (ACMMP.cpp:101-143): frees every device buffer (no double free). */
+void acmmp_destroy(acmmp_ctx *ctx);
+const char *acmmp_status_str(acmmp_status s);
+/* Message of the last error on this context (empty string if none). */
+const char *acmmp_last_error(const acmmp_ctx *ctx);
+int acmmp_abi_version(void);
+
+/* The params member + Set{GeomConsistency,Hierarchy,PlanarPrior}Params
+ * (ACMMP.cpp:548-565).  Copied; may be called again between runs. */
+acmmp_status acmmp_set_params(acmmp_ctx *ctx, const acmmp_params *params);
+
+/* Texture part of CudaSpaceInitialization (ACMMP.cpp:685-712): n = num_images
+ * float grey images (0..255), images[i] is cams[i].height x cams[i].width,
+ * row pitch `pitch_bytes[i]` (NULL -> tightly packed).  cams[0] is the reference. */
+acmmp_status acmmp_upload_views(acmmp_ctx *ctx, int n, const float *const *images,
+                                const size_t *pitch_bytes, const acmmp_camera *cams);
+
+/* Geometric-consistency depth textures (ACMMP.cpp:653-678, 726-751): n depth maps,
+ * depths[i] is h[i] x w[i] row-major (index 0 = reference, as the reference). */
+acmmp_status acmmp_upload_depths(acmmp_ctx *ctx, int n, const float *const *depths,
+                                 const int *w, const int *h);
+
+/* Reference-view state for geom / hierarchy / planar reuse passes
+ * (ACMMP.cpp:772-785, 833-843): planes = P float4 (nx, ny, nz, w) row-major,
+ * costs = P floats (may be NULL -> unchanged).  P = cams[0].width*height. */
+acmmp_status acmmp_set_state(acmmp_ctx *ctx, const float *planes, const float *costs);
+
+/* Hierarchy coarse state scaled_plane_hypotheses (ACMMP.cpp:804-842):
+ * sw*sh float4 row-major. */
+acmmp_status acmmp_set_scaled_state(acmmp_ctx *ctx, const float *planes, int sw, int sh);
+
+/* CudaPlanarPriorInitialization (ACMMP.cpp:847-867) after the host has expanded
+ * labels: prior = P float4 plane params, mask = P labels (0 = no prior). */
+acmmp_status acmmp_set_planar_prior(acmmp_ctx *ctx, const float *prior_planes, const uint32_t *masks);
+
+/* ACMMP::RunPatchMatch (ACMMP.cu:1506-1556) minus the final D2H copy:
+ * init, max_iterations x (black, red), GetDepthandNormal, black/red filter.
+ * `seed` replaces curand_init(clock64(), ...) (ACMMP.cu:684).  Synchronous on
+ * return, like the reference.  Results stay resident in HBM until downloaded. */
+acmmp_status acmmp_run_patchmatch(acmmp_ctx *ctx, uint64_t seed);
+
+/* Same with the schedule exposed (tests / profiling): n_half_sweeps < 0 means
+ * 2*max_iterations; do_post = 0 leaves the raw working state (camera-frame
+ * normal, w = plane distance) instead of (world normal, depth). */
+acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx *ctx, uint64_t seed, int n_half_sweeps, int do_post);
+
+/* The D2H part of RunPatchMatch (ACMMP.cu:1553-1554) + GetPlaneHypothesis/GetCost
+ * (ACMMP.cpp:884-892) in bulk: caller-allocated P float4 / P floats (either may be NULL). */
+acmmp_status acmmp_download(acmmp_ctx *ctx, float *planes, float *costs);
+/* Extra state readback for tests: selected_views bitmasks and pre_costs (either may be NULL). */
+acmmp_status acmmp_download_aux(acmmp_ctx *ctx, uint32_t *selected_views, float *pre_costs);
+
+/* Device-resident outputs (for in-process consumers such as an RCCL depth exchange):
+ * returns device pointers to the row-major planes (float4[P]) and costs (float[P]). */
+acmmp_status acmmp_device_outputs(acmmp_ctx *ctx, void **planes, void **costs);
+
+/* Per-stage device time of the last run, measured with HIP events on the stream
+ * the kernels run on: [init, propagation (all half-sweeps), post]. */
+acmmp_status acmmp_last_timing(const acmmp_ctx *ctx, float ms[3]);
+
+/* RunJBU / JBU::CudaRun (ACMMP.cpp:1071-1122, ACMMP.cu:1558-1649): joint bilateral
+ * upsampling of `coarse` (sw x sh) guided by `ref` (W x H).  imagescale as the
+ * reference computes it: max(H / sh, W / sw) (integer division). */
+acmmp_status acmmp_jbu(acmmp_ctx *ctx, const float *ref, int W, int H, const float *coarse, int sw, int sh,
+                       int imagescale, float *out);
+
+/* ---- test hooks: evaluate the device cost functions on arbitrary inputs ---- */
+/* costs[k*(num_images-1) + v] = ComputeBilateralNCC (ACMMP.cu:405-516) of plane k at
+ * pixel (px[k], py[k]) against source v+1. */
+acmmp_status acmmp_debug_ncc(acmmp_ctx *ctx, int n, const int *px, const int *py, const float *planes,
+                             float *costs);
+/* out[k*(num_images-1) + v] = ComputeGeomConsistencyCost (ACMMP.cu:646-671). */
+acmmp_status acmmp_debug_geom(acmmp_ctx *ctx, int n, const int *px, const int *py, const float *planes,
+                              float *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
