@@ -24,7 +24,8 @@ EXPORTS = [
     "acmmp_abi_version", "acmmp_create", "acmmp_destroy", "acmmp_status_str", "acmmp_last_error",
     "acmmp_set_params", "acmmp_upload_views", "acmmp_upload_depths", "acmmp_set_state",
     "acmmp_set_scaled_state", "acmmp_set_planar_prior", "acmmp_run_patchmatch", "acmmp_run_patchmatch_ex",
-    "acmmp_download", "acmmp_download_aux", "acmmp_device_outputs", "acmmp_last_timing", "acmmp_jbu",
+    "acmmp_download", "acmmp_download_aux", "acmmp_device_outputs", "acmmp_synchronize", "acmmp_last_timing",
+    "acmmp_jbu",
     "acmmp_debug_ncc", "acmmp_debug_geom",
 ]
 
@@ -66,6 +67,7 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_download_aux.argtypes = [vp, vp, vp]
     L.acmmp_device_outputs.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
     L.acmmp_last_timing.argtypes = [vp, vp]
+    L.acmmp_synchronize.argtypes = [vp]
     L.acmmp_jbu.argtypes = [vp, vp, i32, i32, vp, i32, i32, i32, vp]
     L.acmmp_debug_ncc.argtypes = [vp, i32, vp, vp, vp, vp]
     L.acmmp_debug_geom.argtypes = [vp, i32, vp, vp, vp, vp]
@@ -173,6 +175,9 @@ class Context:
         a, b = C.c_void_p(), C.c_void_p()
         self._check(self.L.acmmp_device_outputs(self.h, C.byref(a), C.byref(b)), "device_outputs")
         return a.value, b.value
+
+    def synchronize(self):
+        self._check(self.L.acmmp_synchronize(self.h), "synchronize")
 
     def last_timing(self):
         ms = np.zeros(3, np.float32)

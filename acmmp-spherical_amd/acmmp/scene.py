@@ -39,11 +39,13 @@ def _texture(P: np.ndarray, seed: int, n_waves: int = 48, fmin: float = 2.0, fma
     freqs = rng.uniform(fmin, fmax, size=n_waves)
     phases = rng.uniform(0, 2 * np.pi, size=n_waves)
     amps = 1.0 / np.sqrt(freqs)
-    acc = np.zeros(P.shape[:-1], np.float64)
+    P32 = P.astype(np.float32)
+    acc = np.zeros(P.shape[:-1], np.float32)
     for k in range(n_waves):
-        acc += amps[k] * np.sin(freqs[k] * (P @ dirs[k]) + phases[k])
-    acc /= np.sqrt(np.sum(amps ** 2) / 2.0)
-    return np.clip(127.5 + 60.0 * acc, 0.0, 255.0)
+        acc += np.float32(amps[k]) * np.sin(np.float32(freqs[k]) * (P32 @ dirs[k].astype(np.float32))
+                                            + np.float32(phases[k]))
+    acc /= np.float32(np.sqrt(np.sum(amps ** 2) / 2.0))
+    return np.clip(127.5 + 60.0 * acc.astype(np.float64), 0.0, 255.0)
 
 
 def _look_rotation(yaw: float, pitch: float) -> np.ndarray:

@@ -479,6 +479,13 @@ acmmp_status acmmp_device_outputs(acmmp_ctx* c, void** planes, void** costs) {
     return ACMMP_OK;
 }
 
+acmmp_status acmmp_synchronize(acmmp_ctx* c) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipDeviceSynchronize());
+    return ACMMP_OK;
+}
+
 acmmp_status acmmp_last_timing(const acmmp_ctx* c, float ms[3]) {
     if (!c || !ms) return ACMMP_ERR_INVALID_ARGUMENT;
     for (int i = 0; i < 3; ++i) ms[i] = c->timing[i];

@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X-native ACMMP-Spherical PatchMatch path.
+
+Metric (BASELINE.json): "Mpixels/sec PatchMatch propagation + ms/depth-map, 2000x1500,
+1/2/4/8 GPU".  Workload (SURVEY.md §8d "metric"): one synthetic 2000x1500
+equirectangular (SPHERE) reference view with 4 source views, the reference's
+RunPatchMatch schedule (random init, 3 x black/red propagation, depth+normal, two
+median filters), seed-fixed.  One "step" = one full RunPatchMatch of one reference
+view with inputs already resident in HBM; value = pixel-iterations of all ranks /
+wall time of the timed region (max over ranks), in Mpixel-iterations/s.
+
+N GPUs = N processes, one per GPU (torch.distributed.run); every rank owns its own
+reference view (weak scaling, no data-path collective -- DESIGN.md §7).  Rank
+coordination (barrier, max-over-ranks) uses torch.distributed's gloo backend on the
+host: the engine's HIP runtime is /opt/rocm's, and initialising torch's bundled HIP
+runtime in the same process as well would put two HIP/HSA runtimes in one process.
+
+Extra JSON fields: `roofline` (FP32 compute roof of the propagation kernel, measured
+with HIP events on the kernel's stream; HBM traffic from the committed rocprofv3 PMC
+pass when one exists for this config) and `cpu_baseline` (the CPU oracle on a bounded
+row-band sample of the same view, rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "acmmp-spherical_amd"))
+
+import numpy as np  # noqa: E402
+
+from acmmp import capi, scene, types  # noqa: E402
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
+PEAK_FP32_TFLOPS = 157.3        # FP32 vector (= f32-input MFMA) dense peak
+PEAK_HBM_GBS = 8000.0
+
+# Algorithmic FLOP per pixel-iteration of CheckerboardPropagation:
+# 14 hypotheses x 36 samples x V views x F_HVS + 8.7k shared per-pixel work.
+F_HVS = {"sphere": 100.0, "pinhole": 46.0}
+F_SHARED = 8700.0
+
+
+def algorithmic_flop_per_pixel(model: str, V: int, samples: int = 36) -> float:
+    return 14 * samples * V * F_HVS[model] + F_SHARED
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--width", type=int, default=2000)
+    ap.add_argument("--height", type=int, default=1500)
+    ap.add_argument("--n-src", type=int, default=4)
+    ap.add_argument("--model", choices=["sphere", "pinhole"], default="sphere")
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 -> min(16, os.cpu_count())")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_propagate.json"),
+                    help="rocprofv3 PMC summary giving HBM bytes per propagation launch")
+    return ap.parse_args()
+
+
+def make_scene(args, rank: int):
+    if args.model == "sphere":
+        return scene.sphere_scene(args.width, args.height, n_src=args.n_src, seed=args.seed + 7919 * rank)
+    return scene.pinhole_scene(args.width, args.height, n_src=args.n_src, seed=args.seed + 7919 * rank)
+
+
+def cpu_baseline(args, sc, params, gpu_rate_check=None):
+    """Time the CPU oracle (oracle/, kind "port") on a bounded sample of the same view."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # test/baseline infrastructure only
+
+    oracle.build()
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    prob = oracle.Problem(sc.images, sc.cameras, params)
+    H = args.height
+    # probe: 4 rows to estimate the rate, then bands spread over the image for ~cpu_seconds
+    t0 = time.perf_counter()
+    oracle.run_band(prob, args.seed, H // 2, H // 2 + 4, nthreads=threads)
+    probe = time.perf_counter() - t0
+    per_row = probe / 4.0
+    total_rows = int(max(8, min(H, args.cpu_seconds / max(per_row, 1e-6))))
+    nb = 6
+    rows_per_band = max(2, total_rows // nb)
+    t_sum, rows_done = 0.0, 0
+    for b in range(nb):
+        y0 = int((b + 0.5) * H / nb) - rows_per_band // 2
+        y0 = max(0, min(H - rows_per_band, y0))
+        t0 = time.perf_counter()
+        oracle.run_band(prob, args.seed, y0, y0 + rows_per_band, nthreads=threads)
+        t_sum += time.perf_counter() - t0
+        rows_done += rows_per_band
+    pix_iter = rows_done * args.width * args.iters
+    return {
+        "value": round(pix_iter / t_sum / 1e6, 5),
+        "unit": "Mpixel-iterations/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{nb} bands x {rows_per_band} rows of the same {args.width}x{args.height} {args.model} view "
+                  f"(V={args.n_src}), full init + {args.iters} iterations + post on those rows, "
+                  f"{t_sum:.1f} s CPU wall",
+        "seconds": round(t_sum, 2),
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        dist.init_process_group("gloo")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def allmax(x: float) -> float:
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    sc = make_scene(args, rank)
+    c0 = sc.cameras[0]
+    params = types.default_params(num_images=args.n_src + 1, max_iterations=args.iters,
+                                  depth_min=float(c0["depth_min"]) * 0.6, depth_max=float(c0["depth_max"]) * 1.2)
+    ctx = capi.Context(local_rank)
+    ctx.set_params(params)
+    ctx.upload_views(sc.images, sc.cameras)
+
+    for w in range(args.warmup):
+        ctx.run_patchmatch(args.seed + 100 + w)
+    ctx.synchronize()
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    stage = np.zeros(3)
+    for k in range(args.steps):
+        ctx.run_patchmatch(args.seed + k)
+        tm = ctx.last_timing()
+        stage += [tm["init_ms"], tm["prop_ms"], tm["post_ms"]]
+    ctx.synchronize()
+    barrier()
+    ctx.synchronize()
+    elapsed = time.perf_counter() - t0
+    t_max = allmax(elapsed)
+
+    planes, costs = ctx.download()
+    nan_frac = float(np.isnan(costs).mean())
+    acc = scene.depth_accuracy(planes[..., 3], sc.gt_depth)
+
+    P = args.width * args.height
+    units = P * args.iters * args.steps * world
+    value = units / t_max / 1e6
+    ms_per_step = t_max / args.steps * 1e3
+
+    # roofline of the dominant kernel (k_propagate): mean launch duration from HIP events
+    n_launch = 2 * args.iters * args.steps
+    launch_ms = stage[1] / n_launch
+    rows = min(args.height, 32 * (((args.height // 2) + 15) // 16))
+    pix_per_launch = rows * args.width / 2.0
+    flop_launch = algorithmic_flop_per_pixel(args.model, args.n_src) * pix_per_launch
+    achieved = flop_launch / (launch_ms * 1e-3) / 1e12
+    traffic = None
+    hbm = None
+    if os.path.exists(args.pmc):
+        try:
+            pm = json.load(open(args.pmc))
+            if pm.get("config") == {"width": args.width, "height": args.height, "n_src": args.n_src,
+                                    "model": args.model}:
+                traffic = pm.get("hbm_bytes_per_launch")
+                if traffic:
+                    gbs = traffic / (launch_ms * 1e-3) / 1e9
+                    hbm = {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                           "frac": round(gbs / PEAK_HBM_GBS, 4)}
+        except (OSError, ValueError):
+            pass
+    roofline = {
+        "bound": "valu",
+        "achieved": round(achieved, 3),
+        "peak": PEAK_FP32_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+        "traffic": traffic,
+        "kernel": "k_propagate (CheckerboardPropagation half-sweep)",
+        "launch_ms": round(launch_ms, 4),
+        "flop_per_launch": flop_launch,
+        "hbm": hbm,
+        "note": "FP32 vector peak (equal to the f32 MFMA dense peak); the path has no GEMM-shaped work",
+    }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, sc, params)
+
+    if rank == 0:
+        line = {
+            "metric": "Mpixels/sec PatchMatch propagation + ms/depth-map, 2000x1500, 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "Mpixel-iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "ms_per_depth_map": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (ray-cast textured box room, SPHERE cameras; no dataset reachable)",
+            "config": {"workload": f"RunPatchMatch {args.width}x{args.height} {args.model}, 1 ref + {args.n_src} src, "
+                                   f"{args.iters} iterations, random init, per-GPU reference view",
+                       "width": args.width, "height": args.height, "n_src": args.n_src, "model": args.model,
+                       "iterations": args.iters, "parallelism": f"views-sharded x{world}"},
+            "stages_ms": {"init": round(stage[0] / args.steps, 3), "propagation": round(stage[1] / args.steps, 3),
+                          "post": round(stage[2] / args.steps, 3)},
+            "prop_only_mpix_per_s": round(P * args.iters * world / (stage[1] / args.steps * 1e-3) / 1e6, 3),
+            "quality": {"frac_within_1pct_gt": round(acc, 4), "nan_cost_frac": round(nan_frac, 4)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -136,6 +136,9 @@ acmmp_status acmmp_download_aux(acmmp_ctx *ctx, uint32_t *selected_views, float 
  * returns device pointers to the row-major planes (float4[P]) and costs (float[P]). */
 acmmp_status acmmp_device_outputs(acmmp_ctx *ctx, void **planes, void **costs);
 
+/* Wait for all work of this context's device (hipDeviceSynchronize). */
+acmmp_status acmmp_synchronize(acmmp_ctx *ctx);
+
 /* Per-stage device time of the last run, measured with HIP events on the stream
  * the kernels run on: [init, propagation (all half-sweeps), post]. */
 acmmp_status acmmp_last_timing(const acmmp_ctx *ctx, float ms[3]);

@@ -954,8 +954,24 @@ static void filter_pixel(const Ctx *cx, or_state *st, int px, int py)
 /* rows the reference's checkerboard grid actually covers (ACMMP.cu:1525, :1331-1333) */
 static inline int checker_rows(int H) { int r = 32 * (((H / 2) + 15) / 16); return r < H ? r : H; }
 
+static int run_rows(const or_problem *pb, const or_params *pp, or_state *st, uint64_t seed,
+                    int32_t n_half_sweeps, int32_t do_post, int32_t nthreads, int row0, int row1);
+
 int or_run_patchmatch(const or_problem *pb, const or_params *pp, or_state *st,
                       uint64_t seed, int32_t n_half_sweeps, int32_t do_post, int32_t nthreads)
+{
+    return run_rows(pb, pp, st, seed, n_half_sweeps, do_post, nthreads, 0, pb->cams[0].height);
+}
+
+/* Bounded CPU-baseline sample: the same per-pixel work restricted to rows [row0, row1). */
+int or_run_band(const or_problem *pb, const or_params *pp, or_state *st, uint64_t seed,
+                int32_t n_half_sweeps, int32_t nthreads, int32_t row0, int32_t row1)
+{
+    return run_rows(pb, pp, st, seed, n_half_sweeps, 1, nthreads, row0, row1);
+}
+
+static int run_rows(const or_problem *pb, const or_params *pp, or_state *st, uint64_t seed,
+                    int32_t n_half_sweeps, int32_t do_post, int32_t nthreads, int row0, int row1)
 {
     Ctx cx = { pb, pp, pb->cams[0].width, pb->cams[0].height, pp->num_images - 1, seed };
     const int W = cx.W, H = cx.H;
@@ -972,12 +988,14 @@ int or_run_patchmatch(const or_problem *pb, const or_params *pp, or_state *st,
     uint32_t *sel2 = (uint32_t *)malloc(sizeof(uint32_t) * P);
     if (!rng || !planes2 || !costs2 || !sel2) { free(rng); free(planes2); free(costs2); free(sel2); return 2; }
 
+    if (row0 < 0) row0 = 0;
+    if (row1 > H) row1 = H;
 #pragma omp parallel for schedule(dynamic, 4)
-    for (int y = 0; y < H; ++y)
+    for (int y = row0; y < row1; ++y)
         for (int x = 0; x < W; ++x) init_pixel(&cx, st, x, y, &rng[(size_t)y * W + x]);
 
     if (n_half_sweeps < 0) n_half_sweeps = 2 * pp->max_iterations;
-    const int rows = checker_rows(H);
+    const int rows = checker_rows(H) < row1 ? checker_rows(H) : row1;
     for (int s = 0; s < n_half_sweeps; ++s) {
         const int iter = s / 2, colour = s & 1;
         memcpy(planes2, st->planes, sizeof(float) * 4 * P);
@@ -985,18 +1003,18 @@ int or_run_patchmatch(const or_problem *pb, const or_params *pp, or_state *st,
         memcpy(sel2, st->selected_views, sizeof(uint32_t) * P);
         or_state in = { planes2, costs2, st->pre_costs, sel2 };
 #pragma omp parallel for schedule(dynamic, 2)
-        for (int y = 0; y < rows; ++y)
+        for (int y = row0; y < rows; ++y)
             for (int x = (y + colour) & 1; x < W; x += 2)
                 propagate_pixel(&cx, &in, st, &rng[(size_t)y * W + x], x, y, iter);
     }
 
     if (do_post) {
 #pragma omp parallel for schedule(static)
-        for (int y = 0; y < H; ++y)
+        for (int y = row0; y < row1; ++y)
             for (int x = 0; x < W; ++x) depth_and_normal(&cx, st, x, y);
         for (int colour = 0; colour < 2; ++colour) {
 #pragma omp parallel for schedule(static)
-            for (int y = 0; y < rows; ++y)
+            for (int y = row0; y < rows; ++y)
                 for (int x = (y + colour) & 1; x < W; x += 2) filter_pixel(&cx, st, x, y);
         }
     }
