@@ -43,11 +43,9 @@ struct acmmp_ctx {
     float4* d_dirs = nullptr;
     int dirs_R = -1;
 
-    float* d_tw = nullptr;
-    float* d_twr = nullptr;
-    float* d_tr = nullptr;
-    float* d_tsum = nullptr;
-    size_t table_S = 0;
+    float2* d_sph_row = nullptr;
+    float2* d_sph_col = nullptr;
+    float* d_spatial = nullptr;
 
     float4* d_planes_rm = nullptr;
     float* d_costs_rm = nullptr;
@@ -159,7 +157,7 @@ void acmmp_destroy(acmmp_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     dfree(c->d_cams); dfree(c->d_img); dfree(c->d_dep); dfree(c->d_dirs);
-    dfree(c->d_tw); dfree(c->d_twr); dfree(c->d_tr); dfree(c->d_tsum);
+    dfree(c->d_sph_row); dfree(c->d_sph_col); dfree(c->d_spatial);
     dfree(c->d_planes_rm); dfree(c->d_costs_rm); dfree(c->d_pre); dfree(c->d_sel_rm);
     dfree(c->d_scaled); dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_scratch);
     for (int k = 0; k < 2; ++k) {
@@ -273,9 +271,8 @@ acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images,
             HIP_TRY(c, dalloc(c->d_sel_cs[k], Pc));
             HIP_TRY(c, dalloc(c->d_rng_cs[k], Pc));
         }
-        dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_tw); dfree(c->d_twr); dfree(c->d_tr); dfree(c->d_tsum);
+        dfree(c->d_prior); dfree(c->d_mask);
         dfree(c->d_scratch);
-        c->table_S = 0;
         c->scratch_V = 0;
     }
     return ACMMP_OK;
@@ -372,19 +369,22 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.Pc = static_cast<long long>(c->H) * kp.Wh;
     const size_t Pc = static_cast<size_t>(kp.Pc);
 
+    if (kp.S > 64) return fail(c, ACMMP_ERR_UNSUPPORTED, "more than 64 patch samples (patch_size / radius_increment)");
+    kp.cams = c->d_cams;
     if (c->dirs_R != R) {
-        HIP_TRY(c, dalloc(c->d_dirs, static_cast<size_t>(c->W + 2 * R) * (c->H + 2 * R)));
-        kp.cams = c->d_cams;
-        HIP_TRY(c, launch_dir_table(kp, c->d_dirs, c->stream));
+        if (c->model == kSphere) {
+            dfree(c->d_dirs);
+            HIP_TRY(c, dalloc(c->d_sph_row, static_cast<size_t>(c->H + 2 * R)));
+            HIP_TRY(c, dalloc(c->d_sph_col, static_cast<size_t>(c->W + 2 * R)));
+        } else {
+            HIP_TRY(c, dalloc(c->d_dirs, static_cast<size_t>(c->W + 2 * R) * (c->H + 2 * R)));
+        }
+        HIP_TRY(c, launch_ray_tables(kp, c->d_dirs, c->d_sph_row, c->d_sph_col, c->stream));
         c->dirs_R = R;
     }
-    if (c->table_S != static_cast<size_t>(kp.S)) {
-        HIP_TRY(c, dalloc(c->d_tw, 2 * kp.S * Pc));
-        HIP_TRY(c, dalloc(c->d_twr, 2 * kp.S * Pc));
-        HIP_TRY(c, dalloc(c->d_tr, 2 * kp.S * Pc));
-        HIP_TRY(c, dalloc(c->d_tsum, 3 * 2 * Pc));
-        c->table_S = kp.S;
-    }
+    kp.color_den = 2.0f * p.sigma_color * p.sigma_color;
+    HIP_TRY(c, dalloc(c->d_spatial, static_cast<size_t>(c->model == kSphere ? c->H : 1) * kp.S));
+    HIP_TRY(c, launch_spatial_table(kp, c->d_spatial, c->stream));
     if (c->scratch_V != static_cast<size_t>(kp.V)) {
         HIP_TRY(c, dalloc(c->d_scratch, 8 * static_cast<size_t>(kp.V) * Pc));
         c->scratch_V = kp.V;
@@ -393,7 +393,9 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.img = c->d_img;
     kp.dep = c->d_dep;
     kp.dirs = c->d_dirs;
-    kp.tw = c->d_tw; kp.twr = c->d_twr; kp.tr = c->d_tr; kp.tsum = c->d_tsum;
+    kp.sph_row = c->d_sph_row;
+    kp.sph_col = c->d_sph_col;
+    kp.spatial = c->d_spatial;
     kp.planes_rm = c->d_planes_rm; kp.costs_rm = c->d_costs_rm; kp.pre_rm = c->d_pre; kp.sel_rm = c->d_sel_rm;
     kp.scaled = c->d_scaled; kp.prior = c->d_prior; kp.mask = c->d_mask;
     for (int k = 0; k < 2; ++k) {
@@ -416,7 +418,6 @@ acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx* c, uint64_t seed, int n_half_swe
     const size_t Pc = static_cast<size_t>(kp.Pc);
     hipStream_t s = c->stream;
     HIP_TRY(c, hipEventRecord(c->ev[0], s));
-    HIP_TRY(c, launch_prepare(kp, s));
     HIP_TRY(c, launch_init(kp, s));
     // rows outside the reference's checkerboard grid are never rewritten: keep both buffers equal
     int cur[2] = {0, 0};
@@ -534,7 +535,6 @@ static acmmp_status debug_eval(acmmp_ctx* c, int which, int n, const int* px, co
     if (e == hipSuccess) e = hipMemcpy(dx, px, sizeof(int) * n, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(dy, py, sizeof(int) * n, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(dp, planes, sizeof(float4) * n, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = launch_prepare(kp, c->stream);
     if (e == hipSuccess) e = launch_debug(kp, which, n, dx, dy, dp, dout, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(float) * nout, hipMemcpyDeviceToHost);

@@ -6,8 +6,10 @@
 //  * reference ray table `dirs`: float4 per pixel of the reference view, padded by
 //    the patch radius (PixelToDir, ACMMP.cu:119-134, evaluated once per view
 //    instead of per sample);
-//  * per-pixel patch tables (bilateral weight w, w*ref, ref texel) colour-split,
-//    sample-major, so a wave reads them coalesced;
+//  * SPHERE rays are separable: per-row (sin, cos) of latitude and per-column (sin, cos)
+//    of longitude (a few KB, cache resident) give PixelToDir's exact bits with two
+//    multiplies; the bilateral spatial term per (row, sample) is a small table too, and
+//    each lane keeps its pixel's 36 bilateral weights in LDS for the whole launch;
 //  * working state colour-split (black = (x+y) even, red = odd), each colour
 //    row-major over (H, ceil(W/2)); planes and costs double-buffered per colour so
 //    a half-sweep reads the kernel-entry snapshot of its own colour;
@@ -53,11 +55,11 @@ struct KParams {
     const DevCam* cams;
     const float* img;
     const float* dep;
-    const float4* dirs;
-    const float* tw;                // [2][S][Pc]  bilateral weight
-    const float* twr;               // [2][S][Pc]  weight * ref texel
-    const float* tr;                // [2][S][Pc]  ref texel
-    const float* tsum;              // [2][3][Pc]  SPHERE: sum_bw, sum_ref, sum_ref_ref
+    const float4* dirs;             // PINHOLE ray table, (W+2R) x (H+2R)
+    const float2* sph_row;          // SPHERE (sin, cos) latitude, rows -R .. H+R-1
+    const float2* sph_col;          // SPHERE (sin, cos) longitude, cols -R .. W+R-1
+    const float* spatial;           // [(SPHERE ? H : 1)][S]: -dist / (2 sigma_s^2) (ACMMP.cu:398-403)
+    float color_den;                // 2 * sigma_color^2
     float4* planes_rm;              // persistent row-major state
     float* costs_rm;
     float* pre_rm;
@@ -80,8 +82,8 @@ struct SweepOut {
 };
 
 // Host-side launchers (kernels.hip).
-hipError_t launch_prepare(const KParams& kp, hipStream_t s);
-hipError_t launch_dir_table(const KParams& kp, float4* dirs, hipStream_t s);
+hipError_t launch_ray_tables(const KParams& kp, float4* dirs, float2* sph_row, float2* sph_col, hipStream_t s);
+hipError_t launch_spatial_table(const KParams& kp, float* spatial, hipStream_t s);
 hipError_t launch_init(const KParams& kp, hipStream_t s);
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s);
 hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s);

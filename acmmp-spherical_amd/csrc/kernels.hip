@@ -16,6 +16,8 @@
 //    run (they depend only on the reference image), so no exp() runs per sample;
 //  * current-hypothesis and refinement costs are evaluated only for views some
 //    lane of the wave selected (zero-weight views add exactly +0 in the reference).
+#include <algorithm>
+
 #include "detmath.h"
 #include "engine.h"
 
@@ -171,27 +173,22 @@ __device__ __forceinline__ float texel_padded(const float* img, int pitch, int W
     return img[static_cast<long long>(clampi(iy, 0, H - 1) + 1) * pitch + clampi(ix, 0, W - 1) + 1];
 }
 
-// tex2D(img, x+0.5, y+0.5) with fp32 bilinear weights and clamp addressing.  The one-texel
-// replicated border makes (ix, ix+1) valid for ix in [-1, W-1], which equals clamping both.
-__device__ __forceinline__ float bilinear_padded(const float* img, int pitch, int W, int H, float x, float y) {
-    const float fx = floorf(x), fy = floorf(y);
-    const float a = x - fx, b = y - fy;
-    const int ix = clampi(f2i_sat(fx), -1, W - 1);
-    const int iy = clampi(f2i_sat(fy), -1, H - 1);
-    const float* p0 = img + static_cast<long long>(iy + 1) * pitch + (ix + 1);
-    const float t00 = p0[0], t10 = p0[1], t01 = p0[pitch], t11 = p0[pitch + 1];
-    const float r0 = fmaf(a, t10 - t00, t00);
-    const float r1 = fmaf(a, t11 - t01, t01);
-    return fmaf(b, r1 - r0, r0);
-}
-
 __device__ __forceinline__ float texel_plain(const float* img, int W, int H, int ix, int iy) {
     return img[static_cast<long long>(clampi(iy, 0, H - 1)) * W + clampi(ix, 0, W - 1)];
 }
 
 // ------------------------------------------------------------------ helpers over KParams
 
+// Reference-camera ray of pixel (x, y), |x - px|, |y - py| <= R (PixelToDir, ACMMP.cu:119-134).
+// SPHERE: (cos lat * sin lon, -sin lat, cos lat * cos lon) from the separable tables -- the same
+// two products PixelToDir rounds.  PINHOLE: the precomputed table.
+template <int MODEL>
 __device__ __forceinline__ float4 ray_at(const KParams& kp, int x, int y) {
+    if (MODEL == kSphere) {
+        const float2 r = kp.sph_row[y + kp.R];
+        const float2 c = kp.sph_col[x + kp.R];
+        return make_float4(r.y * c.x, -r.x, r.y * c.y, 0.0f);
+    }
     return kp.dirs[static_cast<long long>(y + kp.R) * kp.dpitch + (x + kp.R)];
 }
 __device__ __forceinline__ long long cs_index(const KParams& kp, int x, int y) {
@@ -199,35 +196,76 @@ __device__ __forceinline__ long long cs_index(const KParams& kp, int x, int y) {
 }
 __device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// ComputeBilateralWeight, ACMMP.cu:398-403
-__device__ __forceinline__ float bilateral_weight(float dx, float dy, float pix, float center, float ss, float sc) {
-    const float sd = sqrtf(fmaf(dy, dy, dx * dx));
-    const float cd = fabsf(pix - center);
-    return det_exp((-sd) / (2.0f * ss * ss) - cd / (2.0f * sc * sc));
+// ------------------------------------------------------------------ NCC over a chunk of views
+
+// Per-pixel patch context: the lane's bilateral weights live in LDS (`lw[s * stride]`),
+// ACMMP.cu:436-486; SPHERE's weight sums are hypothesis- and view-independent.
+struct Patch {
+    const float* lw;
+    int stride;
+    float center;                   // reference texel at the pixel
+    float sbw, sref, srr;           // SPHERE: sum_bw, sum_ref, sum_ref_ref over all samples
+};
+
+typedef float float2u __attribute__((ext_vector_type(2), aligned(4)));
+
+// tex2D(img, x+0.5, y+0.5) with fp32 bilinear weights and clamp addressing.  The one-texel
+// replicated border makes (ix, ix+1) valid for ix in [-1, W-1], which equals clamping both,
+// and lets each row of the footprint be one 8-byte load.
+__device__ __forceinline__ float bilinear_pair(const float* img, int pitch, int W, int H, float x, float y) {
+    const float fx = floorf(x), fy = floorf(y);
+    const float a = x - fx, b = y - fy;
+    const int ix = clampi(f2i_sat(fx), -1, W - 1);
+    const int iy = clampi(f2i_sat(fy), -1, H - 1);
+    const float* p0 = img + static_cast<long long>(iy + 1) * pitch + (ix + 1);
+    const float2u top = *reinterpret_cast<const float2u*>(p0);
+    const float2u bot = *reinterpret_cast<const float2u*>(p0 + pitch);
+    const float r0 = fmaf(a, top.y - top.x, top.x);
+    const float r1 = fmaf(a, bot.y - bot.x, bot.x);
+    return fmaf(b, r1 - r0, r0);
 }
 
-// ------------------------------------------------------------------ NCC over a chunk of views
+// Fill the lane's LDS weights: w_s = exp(spatial_s - |ref_s - center| / (2 sigma_c^2)).
+template <int MODEL>
+__device__ __forceinline__ Patch make_patch(const KParams& kp, int px, int py, float* lw, int stride) {
+    const DevCam& rc = kp.cams[0];
+    const float* ref = kp.img + rc.img_off;
+    Patch pt;
+    pt.lw = lw;
+    pt.stride = stride;
+    pt.center = texel_padded(ref, rc.img_pitch, rc.W, rc.H, px, py);
+    pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f;
+    const float* sp = kp.spatial + (MODEL == kSphere ? static_cast<long long>(py) * kp.S : 0);
+    int s = 0;
+    for (int i = -kp.R; i <= kp.R; i += kp.inc) {
+        for (int j = -kp.R; j <= kp.R; j += kp.inc, ++s) {
+            const float r = texel_padded(ref, rc.img_pitch, rc.W, rc.H, px + i, py + j);
+            const float w = det_exp(sp[s] - fabsf(r - pt.center) / kp.color_den);
+            lw[s * stride] = w;
+            if (MODEL == kSphere) {
+                pt.sbw += w;
+                pt.sref = fmaf(w, r, pt.sref);
+                pt.srr = fmaf(w * r, r, pt.srr);
+            }
+        }
+    }
+    return pt;
+}
 
 // ComputeBilateralNCC (ACMMP.cu:405-516) of plane `ph` at pixel (px, py) against the
 // source views vlist[0..nv) (wave-uniform camera indices 1..N-1), sample-outer.
 template <int MODEL, int VB>
-__device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, long long tix, long long six, float4 ph,
+__device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv, float (&cost)[VB]) {
     const DevCam& rc = kp.cams[0];
+    const float* ref = kp.img + rc.img_off;
     float sbw[VB], sref[VB], srr[VB], ssrc[VB], sss[VB], srs[VB];
     bool cval[VB];
-    const long long Pc = kp.Pc;
-    const float4 dc = ray_at(kp, px, py);
+    const float4 dc = ray_at<MODEL>(kp, px, py);
     const float3 Pc3 = world_point_ray<MODEL>(rc, px, py, depth_from_plane(ph, dc), dc);
-    float s_bw0 = 0.f, s_ref0 = 0.f, s_rr0 = 0.f;
-    if (MODEL == kSphere) {
-        s_bw0 = kp.tsum[six];
-        s_ref0 = kp.tsum[six + Pc];
-        s_rr0 = kp.tsum[six + 2 * Pc];
-    }
 #pragma unroll
     for (int v = 0; v < VB; ++v) {
-        sbw[v] = s_bw0; sref[v] = s_ref0; srr[v] = s_rr0;
+        sbw[v] = pt.sbw; sref[v] = pt.sref; srr[v] = pt.srr;
         ssrc[v] = 0.f; sss[v] = 0.f; srs[v] = 0.f;
         cval[v] = true;
         if (MODEL == kPinhole && v < nv) {
@@ -242,12 +280,11 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, lon
     for (int i = -R; i <= R; i += inc) {
         for (int j = -R; j <= R; j += inc, ++s) {
             const int rx = px + i, ry = py + j;
-            const float4 d = ray_at(kp, rx, ry);
+            const float4 d = ray_at<MODEL>(kp, rx, ry);
             const float3 P = world_point_ray<MODEL>(rc, rx, ry, depth_from_plane(ph, d), d);
-            const long long ti = tix + static_cast<long long>(s) * Pc;
-            const float w = kp.tw[ti];
-            const float wr = kp.twr[ti];
-            const float r = (MODEL == kPinhole) ? kp.tr[ti] : 0.f;
+            const float w = pt.lw[s * pt.stride];
+            const float r = texel_padded(ref, rc.img_pitch, rc.W, rc.H, rx, ry);
+            const float wr = w * r;
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
                 if (v < nv) {
@@ -262,7 +299,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, lon
                         ok = !(sx < 0.0f || sx >= c.Wf || sy < 0.0f || sy >= c.Hf);
                     }
                     if (ok) {
-                        const float sp = bilinear_padded(kp.img + c.img_off, c.img_pitch, c.W, c.H, sx, sy);
+                        const float sp = bilinear_pair(kp.img + c.img_off, c.img_pitch, c.W, c.H, sx, sy);
                         if (MODEL == kPinhole) {
                             sbw[v] += w;
                             sref[v] = fmaf(w, r, sref[v]);
@@ -379,8 +416,8 @@ __device__ __forceinline__ float4 perturbed_normal(float4 v, float4 n, Rng& rs, 
 
 // Evaluate all source views of plane `ph` and hand each cost to f(view0, cost) in view order.
 template <int MODEL, int VB, typename F>
-__device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py, long long tix, long long six,
-                                              float4 ph, uint32_t wave_mask, F&& f) {
+__device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
+                                              uint32_t wave_mask, F&& f) {
     int v = 0;
     const int V = kp.V;
     while (true) {
@@ -400,7 +437,7 @@ __device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py,
         }
         if (nv == 0) break;
         float cost[VB];
-        ncc_chunk<MODEL, VB>(kp, px, py, tix, six, ph, vlist, nv, cost);
+        ncc_chunk<MODEL, VB>(kp, px, py, pt, ph, vlist, nv, cost);
 #pragma unroll
         for (int k = 0; k < VB; ++k)
             if (k < nv) f(vlist[k] - 1, cost[k]);
@@ -424,58 +461,56 @@ __global__ void k_pad_image(const float* __restrict__ src, size_t pitch, int W, 
         src[static_cast<long long>(clampi(y, 0, H - 1)) * pitch + clampi(x, 0, W - 1)];
 }
 
-__global__ void k_dir_table(const KParams kp, float4* __restrict__ dirs) {
+// PixelToDir tables of the reference camera (ACMMP.cu:119-134), evaluated once per view.
+__global__ void k_ray_tables(const KParams kp, float4* __restrict__ dirs, float2* __restrict__ sph_row,
+                             float2* __restrict__ sph_col) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y * blockDim.y + threadIdx.y;
     const int TW = kp.W + 2 * kp.R, TH = kp.H + 2 * kp.R;
+    const DevCam& c = kp.cams[0];
+    if (kp.model == kSphere) {
+        if (y == 0 && x < TW) {
+            const float lon = (static_cast<float>(x - kp.R) - c.cx) / static_cast<float>(c.W) * 2.0f * kCudartPiF;
+            float sl, cl;
+            det_sincos(lon, &sl, &cl);
+            sph_col[x] = make_float2(sl, cl);
+        }
+        if (y == 1 && x < TH) {
+            const float lat = -(static_cast<float>(x - kp.R) - c.cy) / static_cast<float>(c.H) * kCudartPiF;
+            float sa, ca;
+            det_sincos(lat, &sa, &ca);
+            sph_row[x] = make_float2(sa, ca);
+        }
+        return;
+    }
     if (x >= TW || y >= TH) return;
-    const float3 d = pixel_to_dir(kp.cams[0], x - kp.R, y - kp.R);
+    const float3 d = pixel_to_dir(c, x - kp.R, y - kp.R);
     dirs[static_cast<long long>(y) * kp.dpitch + x] = make_float4(d.x, d.y, d.z, 0.0f);
 }
 
-// Per-pixel patch tables (colour-split): w, w*ref, ref for each of the S samples, plus the
-// hypothesis-independent SPHERE sums.  ACMMP.cu:436-493.
-template <int MODEL>
-__global__ void k_prepare(const KParams kp, float* __restrict__ tw, float* __restrict__ twr, float* __restrict__ tr,
-                          float* __restrict__ tsum) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y * blockDim.y + threadIdx.y;
-    const int colour = blockIdx.z;
-    const int x = 2 * k + ((y + colour) & 1);
-    if (x >= kp.W || y >= kp.H) return;
+// Spatial half of ComputeBilateralWeight (ACMMP.cu:398-403, 436-486): -|d| / (2 sigma_s^2) per
+// sample, per row for SPHERE (angular distances depend on the latitude).
+__global__ void k_spatial(const KParams kp, float* __restrict__ spatial) {
+    const int y = blockIdx.x * blockDim.x + threadIdx.x;
+    const int rows = kp.model == kSphere ? kp.H : 1;
+    if (y >= rows) return;
     const DevCam& rc = kp.cams[0];
-    const long long Pc = kp.Pc;
-    const long long tix = static_cast<long long>(colour) * kp.S * Pc + static_cast<long long>(y) * kp.Wh + k;
-    const float* ref = kp.img + rc.img_off;
     float scale_x = 1.0f, scale_y = 1.0f, sig = kp.sigma_spatial;
-    if (MODEL == kSphere) {
+    if (kp.model == kSphere) {
         const float lat_c = -(static_cast<float>(y) - rc.cy) / static_cast<float>(rc.H) * kCudartPiF;
         scale_x = (2.0f * kCudartPiF / static_cast<float>(rc.W)) * det_cos(lat_c);
         scale_y = (kCudartPiF / static_cast<float>(rc.H));
         sig = kp.sigma_spatial * (kCudartPiF / static_cast<float>(rc.H));
     }
-    const float center = texel_padded(ref, rc.img_pitch, rc.W, rc.H, x, y);
-    float sbw = 0.f, sref = 0.f, srr = 0.f;
     int s = 0;
     for (int i = -kp.R; i <= kp.R; i += kp.inc) {
         for (int j = -kp.R; j <= kp.R; j += kp.inc, ++s) {
-            const float r = texel_padded(ref, rc.img_pitch, rc.W, rc.H, x + i, y + j);
-            const float dx = MODEL == kSphere ? static_cast<float>(i) * scale_x : static_cast<float>(i);
-            const float dy = MODEL == kSphere ? static_cast<float>(j) * scale_y : static_cast<float>(j);
-            const float w = bilateral_weight(dx, dy, r, center, sig, kp.sigma_color);
-            const float wr = w * r;
-            tw[tix + s * Pc] = w;
-            twr[tix + s * Pc] = wr;
-            tr[tix + s * Pc] = r;
-            sbw += w;
-            sref = fmaf(w, r, sref);
-            srr = fmaf(wr, r, srr);
+            const float dx = kp.model == kSphere ? static_cast<float>(i) * scale_x : static_cast<float>(i);
+            const float dy = kp.model == kSphere ? static_cast<float>(j) * scale_y : static_cast<float>(j);
+            const float sd = sqrtf(fmaf(dy, dy, dx * dx));
+            spatial[static_cast<long long>(y) * kp.S + s] = (-sd) / (2.0f * sig * sig);
         }
     }
-    const long long si = static_cast<long long>(colour) * 3 * Pc + static_cast<long long>(y) * kp.Wh + k;
-    tsum[si] = sbw;
-    tsum[si + Pc] = sref;
-    tsum[si + 2 * Pc] = srr;
 }
 
 // ------------------------------------------------------------------ initial cost
@@ -491,12 +526,11 @@ __device__ __forceinline__ void sort_small(float* d, int n) {
 
 // ComputeMultiViewInitialCostandSelectedViews, ACMMP.cu:519-556
 template <int MODEL, int VB>
-__device__ float initial_cost(const KParams& kp, int px, int py, long long tix, long long six, float4 ph,
-                             uint32_t* sel) {
+__device__ float initial_cost(const KParams& kp, int px, int py, const Patch& pt, float4 ph, uint32_t* sel) {
     float cv[kMaxViews], cvc[kMaxViews];
     int nvalid = 0;
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
-    for_all_views<MODEL, VB>(kp, px, py, tix, six, ph, all, [&](int v, float c) {
+    for_all_views<MODEL, VB>(kp, px, py, pt, ph, all, [&](int v, float c) {
         cv[v] = c;
         cvc[v] = c;
         if (c < 2.0f) nvalid++;
@@ -538,11 +572,12 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
     const long long center = static_cast<long long>(y) * kp.W + x;
     const int colour = (x + y) & 1;
     const long long ci = cs_index(kp, x, y);
-    const long long tix = static_cast<long long>(colour) * kp.S * kp.Pc + ci;
-    const long long six = static_cast<long long>(colour) * 3 * kp.Pc + ci;
+    extern __shared__ float lds_w[];
+    const int tid = threadIdx.y * blockDim.x + threadIdx.x;
+    const Patch pt = make_patch<MODEL>(kp, x, y, lds_w + tid, blockDim.x * blockDim.y);
     Rng rs;
     rs.init(kp.seed_lo, kp.seed_hi, static_cast<uint32_t>(center), 0u);
-    const float4 dc = ray_at(kp, x, y);
+    const float4 dc = ray_at<MODEL>(kp, x, y);
     float4 ph;
     float cost;
     uint32_t sel = 0;
@@ -550,7 +585,7 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
         const float depth = fmaf(rs.uniform(), kp.depth_max - kp.depth_min, kp.depth_min);
         ph = random_normal(dc, rs);
         ph.w = dist_to_origin(dc, depth, ph);
-        cost = initial_cost<MODEL, VB>(kp, x, y, tix, six, ph, &sel);
+        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel);
     } else if (kp.planar) {
         if (kp.mask[center] > 0 && kp.costs_rm[center] >= 0.1f) {
             const float perturbation = 0.02f;
@@ -566,7 +601,7 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
             const float depth = ph.w;
             ph.w = dist_to_origin(dc, depth, ph);
         }
-        cost = initial_cost<MODEL, VB>(kp, x, y, tix, six, ph, &sel);
+        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel);
     } else if (kp.upsample) {
         const float scale = static_cast<float>(1.0 * static_cast<double>(kp.scaled_cols) / static_cast<double>(kp.W));
         const float sigmad = 0.50f, sigmar = 25.5f;
@@ -600,16 +635,16 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
         normalize3(nx, ny, nz);
         const float4 cur = kp.planes_rm[center];
         uint32_t sel0;
-        kp.pre_rm[center] = initial_cost<MODEL, VB>(kp, x, y, tix, six, cur, &sel0);
+        kp.pre_rm[center] = initial_cost<MODEL, VB>(kp, x, y, pt, cur, &sel0);
         ph = to_ref(rc, make_float4(nx, ny, nz, 0.0f));
         ph.w = dist_to_origin(dc, cur.w, ph);
-        cost = initial_cost<MODEL, VB>(kp, x, y, tix, six, ph, &sel);
+        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel);
     } else {
         ph = kp.hier ? kp.scaled[center] : kp.planes_rm[center];
         ph = to_ref(rc, ph);
         const float depth = ph.w;
         ph.w = dist_to_origin(dc, depth, ph);
-        cost = initial_cost<MODEL, VB>(kp, x, y, tix, six, ph, &sel);
+        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel);
     }
     kp.plane_cs[colour][ci] = ph;
     kp.cost_cs[colour][ci] = cost;
@@ -639,10 +674,11 @@ __global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int c
     const int width = kp.W, height = kp.H, V = kp.V;
     const long long Pc = kp.Pc;
     const long long ci = static_cast<long long>(py) * kp.Wh + kx;
-    const long long tix = static_cast<long long>(colour) * kp.S * Pc + ci;
-    const long long six = static_cast<long long>(colour) * 3 * Pc + ci;
     const long long center = static_cast<long long>(py) * width + px;
-    const float4 dc = ray_at(kp, px, py);
+    extern __shared__ float lds_w[];
+    const Patch pt = make_patch<MODEL>(kp, px, py, lds_w + threadIdx.y * blockDim.x + threadIdx.x,
+                                       blockDim.x * blockDim.y);
+    const float4 dc = ray_at<MODEL>(kp, px, py);
     Rng rs;
     rs.init(kp.seed_lo, kp.seed_hi, static_cast<uint32_t>(center), kp.rng_cs[colour][ci]);
 
@@ -751,7 +787,7 @@ __global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int c
         const bool f = flag[d];
         if (f) nb = plane_at(kp, pos[d]);
         if (f) {
-            for_all_views<MODEL, VB>(kp, px, py, tix, six, nb, all, [&](int v, float c) {
+            for_all_views<MODEL, VB>(kp, px, py, pt, nb, all, [&](int v, float c) {
                 scr[(static_cast<long long>(d) * V + v) * Pc + ci] = c;
             });
         } else {
@@ -847,7 +883,7 @@ __global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int c
     const uint32_t wmask = wave_or(temp_sel);
     float4 cur_plane = kp.plane_cs[colour][ci];
     float cost_now = 0.0f;
-    for_all_views<MODEL, VB>(kp, px, py, tix, six, cur_plane, wmask, [&](int v, float c) {
+    for_all_views<MODEL, VB>(kp, px, py, pt, cur_plane, wmask, [&](int v, float c) {
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
             if (kp.geom) cost_now = fmaf(w, fmaf(0.2f, geom_cost<MODEL>(kp, v + 1, cur_plane, px, py, dc), c), cost_now);
@@ -990,7 +1026,7 @@ __global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int c
             float4 tp = (i == 1 || i == 2) ? n_rand : (i == 3 ? n_pert : p0);
             tp.w = dist_to_origin(dc, dep, tp);
             float temp_cost = 0.0f;
-            for_all_views<MODEL, VB>(kp, px, py, tix, six, tp, wmask, [&](int v, float c) {
+            for_all_views<MODEL, VB>(kp, px, py, pt, tp, wmask, [&](int v, float c) {
                 const float w = vw_get(vwp, v);
                 if (w > 0.0f) {
                     if (kp.geom) temp_cost = fmaf(w, fmaf(0.1f, geom_cost<MODEL>(kp, v + 1, tp, px, py, dc), c), temp_cost);
@@ -1030,6 +1066,7 @@ __global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int c
 // ------------------------------------------------------------------ kernels: post
 
 // GetDepthandNormal (ACMMP.cu:1351-1364) fused with the colour-split -> row-major merge.
+template <int MODEL>
 __global__ void k_merge(const KParams kp, const int do_post) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y * blockDim.y + threadIdx.y;
@@ -1039,7 +1076,7 @@ __global__ void k_merge(const KParams kp, const int do_post) {
     const long long center = static_cast<long long>(y) * kp.W + x;
     float4 ph = kp.plane_cs[colour][ci];
     if (do_post) {
-        ph.w = depth_from_plane(ph, ray_at(kp, x, y));
+        ph.w = depth_from_plane(ph, ray_at<MODEL>(kp, x, y));
         ph = to_world(kp.cams[0], ph);
     }
     kp.planes_rm[center] = ph;
@@ -1131,14 +1168,15 @@ __global__ void k_debug(const KParams kp, int which, int n, const int* __restric
     const int x = qx[q], y = qy[q];
     const float4 ph = planes[q];
     const int colour = (x + y) & 1;
-    const long long tix = static_cast<long long>(colour) * kp.S * kp.Pc + cs_index(kp, x, y);
-    const long long six = static_cast<long long>(colour) * 3 * kp.Pc + cs_index(kp, x, y);
+    (void)colour;
+    extern __shared__ float lds_w[];
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     if (which == 0) {
-        for_all_views<MODEL, VB>(kp, x, y, tix, six, ph, all,
+        const Patch pt = make_patch<MODEL>(kp, x, y, lds_w + threadIdx.x, blockDim.x);
+        for_all_views<MODEL, VB>(kp, x, y, pt, ph, all,
                                  [&](int v, float c) { out[static_cast<long long>(q) * kp.V + v] = c; });
     } else {
-        const float4 dc = ray_at(kp, x, y);
+        const float4 dc = ray_at<MODEL>(kp, x, y);
         for (int v = 0; v < kp.V; ++v)
             out[static_cast<long long>(q) * kp.V + v] = geom_cost<MODEL>(kp, v + 1, ph, x, y, dc);
     }
@@ -1155,20 +1193,20 @@ hipError_t launch_pad_image(const float* src, size_t pitch_floats, int W, int H,
     return hipGetLastError();
 }
 
-hipError_t launch_dir_table(const KParams& kp, float4* dirs, hipStream_t s) {
-    dim3 blk(64, 4), grd(cdiv(kp.W + 2 * kp.R, 64), cdiv(kp.H + 2 * kp.R, 4));
-    k_dir_table<<<grd, blk, 0, s>>>(kp, dirs);
+hipError_t launch_ray_tables(const KParams& kp, float4* dirs, float2* sph_row, float2* sph_col, hipStream_t s) {
+    if (kp.model == kSphere) {
+        const int n = std::max(kp.W, kp.H) + 2 * kp.R;
+        k_ray_tables<<<dim3(cdiv(n, 256), 2), dim3(256, 1), 0, s>>>(kp, dirs, sph_row, sph_col);
+    } else {
+        dim3 blk(64, 4), grd(cdiv(kp.W + 2 * kp.R, 64), cdiv(kp.H + 2 * kp.R, 4));
+        k_ray_tables<<<grd, blk, 0, s>>>(kp, dirs, sph_row, sph_col);
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_prepare(const KParams& kp, hipStream_t s) {
-    dim3 blk(64, 4), grd(cdiv(kp.Wh, 64), cdiv(kp.H, 4), 2);
-    float* tw = const_cast<float*>(kp.tw);
-    float* twr = const_cast<float*>(kp.twr);
-    float* tr = const_cast<float*>(kp.tr);
-    float* ts = const_cast<float*>(kp.tsum);
-    if (kp.model == kSphere) k_prepare<kSphere><<<grd, blk, 0, s>>>(kp, tw, twr, tr, ts);
-    else k_prepare<kPinhole><<<grd, blk, 0, s>>>(kp, tw, twr, tr, ts);
+hipError_t launch_spatial_table(const KParams& kp, float* spatial, hipStream_t s) {
+    const int rows = kp.model == kSphere ? kp.H : 1;
+    k_spatial<<<cdiv(rows, 64), 64, 0, s>>>(kp, spatial);
     return hipGetLastError();
 }
 
@@ -1195,20 +1233,23 @@ static inline int pick_vb(int V) { return V <= 1 ? 1 : (V <= 2 ? 2 : (V <= 4 ? 4
 
 hipError_t launch_init(const KParams& kp, hipStream_t s) {
     dim3 blk(16, 16), grd(cdiv(kp.W, 16), cdiv(kp.H, 16));
-    ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC><<<grd, blk, 0, s>>>(kp)));
+    const size_t lds = sizeof(float) * kp.S * 256;
+    ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC><<<grd, blk, lds, s>>>(kp)));
     return hipGetLastError();
 }
 
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s) {
     dim3 blk(64, 4), grd(cdiv(kp.Wh, 64), cdiv(kp.rows, 4));
-    ACMMP_DISPATCH(kp.model, kp.V, (k_propagate<M, VBC><<<grd, blk, 0, s>>>(kp, colour, iter, out)));
+    const size_t lds = sizeof(float) * kp.S * 256;
+    ACMMP_DISPATCH(kp.model, kp.V, (k_propagate<M, VBC><<<grd, blk, lds, s>>>(kp, colour, iter, out)));
     return hipGetLastError();
 }
 
 hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s) {
     {
         dim3 blk(64, 4), grd(cdiv(kp.W, 64), cdiv(kp.H, 4));
-        k_merge<<<grd, blk, 0, s>>>(kp, do_post);
+        if (kp.model == kSphere) k_merge<kSphere><<<grd, blk, 0, s>>>(kp, do_post);
+        else k_merge<kPinhole><<<grd, blk, 0, s>>>(kp, do_post);
     }
     if (do_post) {
         dim3 blk(64, 4), grd(cdiv(kp.Wh, 64), cdiv(kp.rows, 4));
@@ -1228,7 +1269,8 @@ hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int s
 hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,
                         float* out, hipStream_t s) {
     dim3 blk(64), grd(cdiv(n, 64));
-    ACMMP_DISPATCH(kp.model, kp.V, (k_debug<M, VBC><<<grd, blk, 0, s>>>(kp, which, n, px, py, planes, out)));
+    const size_t lds = sizeof(float) * kp.S * 64;
+    ACMMP_DISPATCH(kp.model, kp.V, (k_debug<M, VBC><<<grd, blk, lds, s>>>(kp, which, n, px, py, planes, out)));
     return hipGetLastError();
 }
 
