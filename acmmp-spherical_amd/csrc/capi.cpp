@@ -62,8 +62,8 @@ struct acmmp_ctx {
     float* d_cost_cs[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
     uint32_t* d_sel_cs[2] = {nullptr, nullptr};
     uint32_t* d_rng_cs[2] = {nullptr, nullptr};
-    float* d_scratch = nullptr;
-    size_t scratch_V = 0;
+    char* d_scratch = nullptr;
+    size_t scratch_bytes = 0;
 
     float timing[3] = {0.f, 0.f, 0.f};
     std::string err;
@@ -273,7 +273,7 @@ acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images,
         }
         dfree(c->d_prior); dfree(c->d_mask);
         dfree(c->d_scratch);
-        c->scratch_V = 0;
+        c->scratch_bytes = 0;
     }
     return ACMMP_OK;
 }
@@ -385,9 +385,18 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.color_den = 2.0f * p.sigma_color * p.sigma_color;
     HIP_TRY(c, dalloc(c->d_spatial, static_cast<size_t>(c->model == kSphere ? c->H : 1) * kp.S));
     HIP_TRY(c, launch_spatial_table(kp, c->d_spatial, c->stream));
-    if (c->scratch_V != static_cast<size_t>(kp.V)) {
-        HIP_TRY(c, dalloc(c->d_scratch, 8 * static_cast<size_t>(kp.V) * Pc));
-        c->scratch_V = kp.V;
+    // half-sweep scratch slab: carve the pieces of engine.h's KParams out of one allocation
+    size_t off[7];
+    {
+        const size_t sizes[6] = {sizeof(float) * 9 * static_cast<size_t>(kp.V) * Pc, sizeof(int) * 8 * Pc,
+                                 sizeof(float4) * 5 * Pc, sizeof(float) * 5 * Pc, sizeof(float) * 5 * Pc,
+                                 sizeof(PixState) * Pc};
+        off[0] = 0;
+        for (int k = 0; k < 6; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
+    }
+    if (c->scratch_bytes < off[6]) {
+        HIP_TRY(c, dalloc(c->d_scratch, off[6]));
+        c->scratch_bytes = off[6];
     }
     kp.cams = c->d_cams;
     kp.img = c->d_img;
@@ -404,7 +413,12 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
         kp.sel_cs[k] = c->d_sel_cs[k];
         kp.rng_cs[k] = c->d_rng_cs[k];
     }
-    kp.scratch = c->d_scratch;
+    kp.hyp_cost = reinterpret_cast<float*>(c->d_scratch + off[0]);
+    kp.nbpos = reinterpret_cast<int*>(c->d_scratch + off[1]);
+    kp.cand = reinterpret_cast<float4*>(c->d_scratch + off[2]);
+    kp.cand_dep = reinterpret_cast<float*>(c->d_scratch + off[3]);
+    kp.cand_cost = reinterpret_cast<float*>(c->d_scratch + off[4]);
+    kp.pst = reinterpret_cast<PixState*>(c->d_scratch + off[5]);
     return ACMMP_OK;
 }
 

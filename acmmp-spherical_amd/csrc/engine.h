@@ -40,6 +40,17 @@ struct DevCam {
     int dep_w, dep_h;
 };
 
+// Per-pixel state handed from k_select to k_eval_ref / k_finish (80 bytes).
+struct PixState {
+    float4 plane_now;               // hypothesis entering PlaneHypothesisRefinement
+    float4 cur_plane;               // plane_hypotheses[center] as of ACMMP.cu:1299
+    uint4 vw;                       // view weights, 4-bit counts packed 8 per word
+    float cost_now, depth_now, cur_cost, restricted_cost;
+    uint32_t cur_sel, flags;        // flags: 1 = prior restricted, 2 = refinement runs
+    float weight_norm;
+    uint32_t pad;
+};
+
 struct KParams {
     int model;                      // kPinhole / kSphere, uniform over all views
     int W, H, Wh, N, V;             // ref size, colour row width ceil(W/2), images, source views
@@ -71,7 +82,13 @@ struct KParams {
     float* cost_cs[2];
     uint32_t* sel_cs[2];
     uint32_t* rng_cs[2];            // Philox draw counter per pixel
-    float* scratch;                 // [8][V][Pc] propagation cost matrix
+    // half-sweep scratch slab (one colour at a time)
+    float* hyp_cost;                // [9][V][Pc] cost vectors of the 8 neighbours + current plane
+    int* nbpos;                     // [8][Pc] picked neighbour (x | y << 16) or -1
+    float4* cand;                   // [5][Pc] refinement candidate planes
+    float* cand_dep;                // [5][Pc] their depths (prior term, ACMMP.cu:912)
+    float* cand_cost;               // [5][Pc] their aggregated costs
+    PixState* pst;                  // [Pc]
     long long Pc;                   // H * Wh
 };
 

@@ -351,11 +351,13 @@ __device__ __forceinline__ float geom_cost(const KParams& kp, int sv, float4 ph,
     return fminf(3.0f, sqrtf(fmaf(drow, drow, dcol * dcol)));
 }
 
-// Views that at least one active lane of the wave needs (mask = per-lane bitmask of views 0..V-1).
-__device__ __forceinline__ uint32_t wave_or(uint32_t mask) {
-    uint32_t r = 0;
-    for (int off = 32; off >= 1; off >>= 1) mask |= __shfl_xor(mask, off);
-    r = mask;
+// Views that at least one ACTIVE lane of the wave needs (mask = per-lane bitmask of views 0..V-1).
+// Ballots only see active lanes, so lanes that already returned cannot drop bits (a shuffle
+// butterfly would route partial results through inactive lanes).
+__device__ __forceinline__ uint32_t wave_or(uint32_t mask, int V) {
+    uint32_t r = 0u;
+    for (int v = 0; v < V; ++v)
+        if (__ballot((mask >> v) & 1u)) r |= 1u << v;
     return uniform_int(static_cast<int>(r));
 }
 
@@ -652,7 +654,19 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
     kp.rng_cs[colour][ci] = rs.n;
 }
 
-// ------------------------------------------------------------------ kernel: CheckerboardPropagation
+// ------------------------------------------------------------------ kernels: CheckerboardPropagation
+//
+// One half-sweep of CheckerboardPropagation (ACMMP.cu:938-1325, launched by Black/RedPixelUpdate
+// :1327-1349) runs as four launches over the pixels of one colour:
+//   k_eval_nb   one lane per (pixel, hypothesis): adaptive neighbour pick of direction h (h < 8)
+//               or the pixel's own plane (h == 8), then its cost vector over all source views
+//   k_select    one lane per pixel: joint view selection, aggregated costs, acceptance, and the
+//               five refinement candidates of PlaneHypothesisRefinement (all RNG draws, in order)
+//   k_eval_ref  one lane per (pixel, candidate): aggregated cost of each valid candidate
+//   k_finish    one lane per pixel: refinement acceptance in candidate order, hierarchy gate, store
+// Intermediate per-pixel state goes through the scratch slab (engine.h).  Same-colour reads see the
+// kernel-entry snapshot: neighbour planes/costs come from the colour's current buffer, the result
+// goes to its other buffer.
 
 __device__ __forceinline__ float cost_at(const KParams& kp, int x, int y) {
     return kp.cost_cs[(x + y) & 1][cs_index(kp, x, y)];
@@ -663,139 +677,221 @@ __device__ __forceinline__ float4 plane_at(const KParams& kp, int pos) {
 }
 __device__ __forceinline__ int packpos(int x, int y) { return x | (y << 16); }
 
-// ACMMP.cu:938-1325 + 1327-1349 for one colour; snapshot semantics.
+// Adaptive checkerboard sampling of one direction (ACMMP.cu:965-1143); returns the packed position
+// or -1 when the direction is unavailable (flag[d] == false).
+__device__ __forceinline__ int pick_neighbour(const KParams& kp, int d, int px, int py) {
+    const int width = kp.W, height = kp.H;
+    float cmin;
+    int cpos;
+    switch (d) {
+    case 1:                                                   // up_far
+        if (!(py > 2)) return -1;
+        cmin = cost_at(kp, px, py - 3); cpos = packpos(px, py - 3);
+        for (int i = 1; i < 11; ++i) if (py > 2 + 2 * i) {
+            const float c = cost_at(kp, px, py - 3 - 2 * i);
+            if (c < cmin) { cmin = c; cpos = packpos(px, py - 3 - 2 * i); }
+        }
+        return cpos;
+    case 3:                                                   // down_far
+        if (!(py < height - 3)) return -1;
+        cmin = cost_at(kp, px, py + 3); cpos = packpos(px, py + 3);
+        for (int i = 1; i < 11; ++i) if (py < height - 3 - 2 * i) {
+            const float c = cost_at(kp, px, py + 3 + 2 * i);
+            if (c < cmin) { cmin = c; cpos = packpos(px, py + 3 + 2 * i); }
+        }
+        return cpos;
+    case 5:                                                   // left_far
+        if (!(px > 2)) return -1;
+        cmin = cost_at(kp, px - 3, py); cpos = packpos(px - 3, py);
+        for (int i = 1; i < 11; ++i) if (px > 2 + 2 * i) {
+            const float c = cost_at(kp, px - 3 - 2 * i, py);
+            if (c < cmin) { cmin = c; cpos = packpos(px - 3 - 2 * i, py); }
+        }
+        return cpos;
+    case 7:                                                   // right_far
+        if (!(px < width - 3)) return -1;
+        cmin = cost_at(kp, px + 3, py); cpos = packpos(px + 3, py);
+        for (int i = 1; i < 11; ++i) if (px < width - 3 - 2 * i) {
+            const float c = cost_at(kp, px + 3 + 2 * i, py);
+            if (c < cmin) { cmin = c; cpos = packpos(px + 3 + 2 * i, py); }
+        }
+        return cpos;
+    case 0:                                                   // up_near (V shape, same colour)
+        if (!(py > 0)) return -1;
+        cmin = cost_at(kp, px, py - 1); cpos = packpos(px, py - 1);
+        for (int i = 0; i < 3; ++i) {
+            if (py > 1 + i && px > i) {
+                const float c = cost_at(kp, px - i, py - 2 - i);
+                if (c < cmin) { cmin = c; cpos = packpos(px - i, py - 2 - i); }
+            }
+            if (py > 1 + i && px < width - 1 - i) {
+                const float c = cost_at(kp, px + i, py - 2 - i);
+                if (c < cmin) { cmin = c; cpos = packpos(px + i, py - 2 - i); }
+            }
+        }
+        return cpos;
+    case 2:                                                   // down_near
+        if (!(py < height - 1)) return -1;
+        cmin = cost_at(kp, px, py + 1); cpos = packpos(px, py + 1);
+        for (int i = 0; i < 3; ++i) {
+            if (py < height - 2 - i && px > i) {
+                const float c = cost_at(kp, px - i, py + 2 + i);
+                if (c < cmin) { cmin = c; cpos = packpos(px - i, py + 2 + i); }
+            }
+            if (py < height - 2 - i && px < width - 1 - i) {
+                const float c = cost_at(kp, px + i, py + 2 + i);
+                if (c < cmin) { cmin = c; cpos = packpos(px + i, py + 2 + i); }
+            }
+        }
+        return cpos;
+    case 4:                                                   // left_near
+        if (!(px > 0)) return -1;
+        cmin = cost_at(kp, px - 1, py); cpos = packpos(px - 1, py);
+        for (int i = 0; i < 3; ++i) {
+            if (px > 1 + i && py > i) {
+                const float c = cost_at(kp, px - 2 - i, py - i);
+                if (c < cmin) { cmin = c; cpos = packpos(px - 2 - i, py - i); }
+            }
+            if (px > 1 + i && py < height - 1 - i) {
+                const float c = cost_at(kp, px - 2 - i, py + i);
+                if (c < cmin) { cmin = c; cpos = packpos(px - 2 - i, py + i); }
+            }
+        }
+        return cpos;
+    default:                                                  // 6: right_near
+        if (!(px < width - 1)) return -1;
+        cmin = cost_at(kp, px + 1, py); cpos = packpos(px + 1, py);
+        for (int i = 0; i < 3; ++i) {
+            if (px < width - 2 - i && py > i) {
+                const float c = cost_at(kp, px + 2 + i, py - i);
+                if (c < cmin) { cmin = c; cpos = packpos(px + 2 + i, py - i); }
+            }
+            if (px < width - 2 - i && py < height - 1 - i) {
+                const float c = cost_at(kp, px + 2 + i, py + i);
+                if (c < cmin) { cmin = c; cpos = packpos(px + 2 + i, py + i); }
+            }
+        }
+        return cpos;
+    }
+}
+
+// Pixel q of the colour grid (row-major over rows x Wh); false when it does not exist.
+__device__ __forceinline__ bool colour_pixel(const KParams& kp, int colour, long long q, int& px, int& py) {
+    py = static_cast<int>(q / kp.Wh);
+    const int k = static_cast<int>(q - static_cast<long long>(py) * kp.Wh);
+    px = 2 * k + ((py + colour) & 1);
+    return py < kp.rows && px < kp.W;
+}
+
+// Cooperative LDS weights for the block's pixels: lane `h` of `nh` lanes of pixel slot `lp`
+// computes samples h, h+nh, ... (ACMMP.cu:436-486); SPHERE sums by the first lane of each pixel.
+template <int MODEL>
+__device__ __forceinline__ void coop_weights(const KParams& kp, bool valid, int px, int py, int lp, int h, int nh,
+                                             float* lw, float* lr, float* lsum) {
+    if (valid) {
+        const DevCam& rc = kp.cams[0];
+        const float* ref = kp.img + rc.img_off;
+        const float center = texel_padded(ref, rc.img_pitch, rc.W, rc.H, px, py);
+        const float* sp = kp.spatial + (MODEL == kSphere ? static_cast<long long>(py) * kp.S : 0);
+        for (int s = h; s < kp.S; s += nh) {
+            const int i = -kp.R + (s / kp.nside) * kp.inc, j = -kp.R + (s % kp.nside) * kp.inc;
+            const float r = texel_padded(ref, rc.img_pitch, rc.W, rc.H, px + i, py + j);
+            lw[lp * kp.S + s] = det_exp(sp[s] - fabsf(r - center) / kp.color_den);
+            lr[lp * kp.S + s] = r;
+        }
+    }
+    __syncthreads();
+    if (MODEL == kSphere && valid && h == 0) {
+        float sbw = 0.f, sref = 0.f, srr = 0.f;
+        for (int s = 0; s < kp.S; ++s) {
+            const float w = lw[lp * kp.S + s], r = lr[lp * kp.S + s];
+            sbw += w;
+            sref = fmaf(w, r, sref);
+            srr = fmaf(w * r, r, srr);
+        }
+        lsum[lp * 3 + 0] = sbw; lsum[lp * 3 + 1] = sref; lsum[lp * 3 + 2] = srr;
+    }
+    __syncthreads();
+}
+
+template <int MODEL>
+__device__ __forceinline__ Patch patch_from_lds(const KParams& kp, int px, int py, int lp, const float* lw,
+                                                const float* lsum) {
+    const DevCam& rc = kp.cams[0];
+    Patch pt;
+    pt.lw = lw + lp * kp.S;
+    pt.stride = 1;
+    pt.center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
+    pt.sbw = MODEL == kSphere ? lsum[lp * 3 + 0] : 0.f;
+    pt.sref = MODEL == kSphere ? lsum[lp * 3 + 1] : 0.f;
+    pt.srr = MODEL == kSphere ? lsum[lp * 3 + 2] : 0.f;
+    return pt;
+}
+
+constexpr int kNbLanes = 9;                 // 8 neighbour directions + the current plane
+constexpr int kNbPix = 28;                  // pixels per 256-lane block (252 lanes used)
+constexpr int kRefLanes = 5;                // refinement candidates (ACMMP.cu:870)
+constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 lanes used)
+
 template <int MODEL, int VB>
-__global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int colour, const int iter,
-                                                   const SweepOut out) {
-    const int kx = blockIdx.x * blockDim.x + threadIdx.x;
-    const int py = blockIdx.y * blockDim.y + threadIdx.y;
-    const int px = 2 * kx + ((py + colour) & 1);
-    if (py >= kp.rows || px >= kp.W) return;
-    const int width = kp.W, height = kp.H, V = kp.V;
+__global__ __launch_bounds__(256) void k_eval_nb(const KParams kp, const int colour) {
+    __shared__ float lw[kNbPix * 64];
+    __shared__ float lr[kNbPix * 64];
+    __shared__ float lsum[kNbPix * 3];
+    const int t = threadIdx.x;
+    const int lp = t / kNbLanes, h = t - lp * kNbLanes;
+    const long long q = static_cast<long long>(blockIdx.x) * kNbPix + lp;
+    int px = 0, py = 0;
+    const bool valid = t < kNbPix * kNbLanes && colour_pixel(kp, colour, q, px, py);
+    coop_weights<MODEL>(kp, valid, px, py, lp, h, kNbLanes, lw, lr, lsum);
+    if (!valid) return;
     const long long Pc = kp.Pc;
-    const long long ci = static_cast<long long>(py) * kp.Wh + kx;
-    const long long center = static_cast<long long>(py) * width + px;
-    extern __shared__ float lds_w[];
-    const Patch pt = make_patch<MODEL>(kp, px, py, lds_w + threadIdx.y * blockDim.x + threadIdx.x,
-                                       blockDim.x * blockDim.y);
+    const long long ci = static_cast<long long>(py) * kp.Wh + (px >> 1);
+    float4 ph;
+    if (h < 8) {
+        const int pos = pick_neighbour(kp, h, px, py);
+        kp.nbpos[h * Pc + ci] = pos;
+        if (pos < 0) return;
+        ph = plane_at(kp, pos);
+    } else {
+        ph = kp.plane_cs[colour][ci];
+    }
+    const Patch pt = patch_from_lds<MODEL>(kp, px, py, lp, lw, lsum);
+    const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
+    float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
+    for_all_views<MODEL, VB>(kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
+}
+
+// Joint view selection, aggregation, acceptance and refinement candidates (ACMMP.cu:1146-1311,
+// 797-874).  `iter` selects the view-selection threshold 0.8 exp(-iter^2 / 90) (:1163).
+template <int MODEL>
+__global__ __launch_bounds__(256) void k_select(const KParams kp, const int colour, const int iter) {
+    const long long q = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+    int px = 0, py = 0;
+    if (!colour_pixel(kp, colour, q, px, py)) return;
+    const int V = kp.V;
+    const long long Pc = kp.Pc;
+    const long long ci = static_cast<long long>(py) * kp.Wh + (px >> 1);
+    const long long center = static_cast<long long>(py) * kp.W + px;
     const float4 dc = ray_at<MODEL>(kp, px, py);
     Rng rs;
     rs.init(kp.seed_lo, kp.seed_hi, static_cast<uint32_t>(center), kp.rng_cs[colour][ci]);
 
-    // ---- adaptive checkerboard sampling :965-1143 (positions packed x | y << 16)
     int pos[8];
     bool flag[8];
 #pragma unroll
-    for (int d = 0; d < 8; ++d) { flag[d] = false; pos[d] = 0; }
-    {
-        float cmin; int cpos;
-        if (py > 2) {                                           // up_far
-            flag[1] = true; cmin = cost_at(kp, px, py - 3); cpos = packpos(px, py - 3);
-            for (int i = 1; i < 11; ++i) if (py > 2 + 2 * i) {
-                const float c = cost_at(kp, px, py - 3 - 2 * i);
-                if (c < cmin) { cmin = c; cpos = packpos(px, py - 3 - 2 * i); }
-            }
-            pos[1] = cpos;
-        }
-        if (py < height - 3) {                                  // down_far
-            flag[3] = true; cmin = cost_at(kp, px, py + 3); cpos = packpos(px, py + 3);
-            for (int i = 1; i < 11; ++i) if (py < height - 3 - 2 * i) {
-                const float c = cost_at(kp, px, py + 3 + 2 * i);
-                if (c < cmin) { cmin = c; cpos = packpos(px, py + 3 + 2 * i); }
-            }
-            pos[3] = cpos;
-        }
-        if (px > 2) {                                           // left_far
-            flag[5] = true; cmin = cost_at(kp, px - 3, py); cpos = packpos(px - 3, py);
-            for (int i = 1; i < 11; ++i) if (px > 2 + 2 * i) {
-                const float c = cost_at(kp, px - 3 - 2 * i, py);
-                if (c < cmin) { cmin = c; cpos = packpos(px - 3 - 2 * i, py); }
-            }
-            pos[5] = cpos;
-        }
-        if (px < width - 3) {                                   // right_far
-            flag[7] = true; cmin = cost_at(kp, px + 3, py); cpos = packpos(px + 3, py);
-            for (int i = 1; i < 11; ++i) if (px < width - 3 - 2 * i) {
-                const float c = cost_at(kp, px + 3 + 2 * i, py);
-                if (c < cmin) { cmin = c; cpos = packpos(px + 3 + 2 * i, py); }
-            }
-            pos[7] = cpos;
-        }
-        if (py > 0) {                                           // up_near (V shape, same colour)
-            flag[0] = true; cmin = cost_at(kp, px, py - 1); cpos = packpos(px, py - 1);
-            for (int i = 0; i < 3; ++i) {
-                if (py > 1 + i && px > i) {
-                    const float c = cost_at(kp, px - i, py - 2 - i);
-                    if (c < cmin) { cmin = c; cpos = packpos(px - i, py - 2 - i); }
-                }
-                if (py > 1 + i && px < width - 1 - i) {
-                    const float c = cost_at(kp, px + i, py - 2 - i);
-                    if (c < cmin) { cmin = c; cpos = packpos(px + i, py - 2 - i); }
-                }
-            }
-            pos[0] = cpos;
-        }
-        if (py < height - 1) {                                  // down_near
-            flag[2] = true; cmin = cost_at(kp, px, py + 1); cpos = packpos(px, py + 1);
-            for (int i = 0; i < 3; ++i) {
-                if (py < height - 2 - i && px > i) {
-                    const float c = cost_at(kp, px - i, py + 2 + i);
-                    if (c < cmin) { cmin = c; cpos = packpos(px - i, py + 2 + i); }
-                }
-                if (py < height - 2 - i && px < width - 1 - i) {
-                    const float c = cost_at(kp, px + i, py + 2 + i);
-                    if (c < cmin) { cmin = c; cpos = packpos(px + i, py + 2 + i); }
-                }
-            }
-            pos[2] = cpos;
-        }
-        if (px > 0) {                                           // left_near
-            flag[4] = true; cmin = cost_at(kp, px - 1, py); cpos = packpos(px - 1, py);
-            for (int i = 0; i < 3; ++i) {
-                if (px > 1 + i && py > i) {
-                    const float c = cost_at(kp, px - 2 - i, py - i);
-                    if (c < cmin) { cmin = c; cpos = packpos(px - 2 - i, py - i); }
-                }
-                if (px > 1 + i && py < height - 1 - i) {
-                    const float c = cost_at(kp, px - 2 - i, py + i);
-                    if (c < cmin) { cmin = c; cpos = packpos(px - 2 - i, py + i); }
-                }
-            }
-            pos[4] = cpos;
-        }
-        if (px < width - 1) {                                   // right_near
-            flag[6] = true; cmin = cost_at(kp, px + 1, py); cpos = packpos(px + 1, py);
-            for (int i = 0; i < 3; ++i) {
-                if (px < width - 2 - i && py > i) {
-                    const float c = cost_at(kp, px + 2 + i, py - i);
-                    if (c < cmin) { cmin = c; cpos = packpos(px + 2 + i, py - i); }
-                }
-                if (px < width - 2 - i && py < height - 1 - i) {
-                    const float c = cost_at(kp, px + 2 + i, py + i);
-                    if (c < cmin) { cmin = c; cpos = packpos(px + 2 + i, py + i); }
-                }
-            }
-            pos[6] = cpos;
-        }
-    }
-
-    // ---- 8 x V cost matrix into the scratch slab [d][v][Pc]
-    const uint32_t all = V >= 32 ? 0xFFFFFFFFu : ((1u << V) - 1u);
-    float* scr = kp.scratch;
     for (int d = 0; d < 8; ++d) {
-        float4 nb = make_float4(0.f, 0.f, 0.f, 0.f);
-        const bool f = flag[d];
-        if (f) nb = plane_at(kp, pos[d]);
-        if (f) {
-            for_all_views<MODEL, VB>(kp, px, py, pt, nb, all, [&](int v, float c) {
-                scr[(static_cast<long long>(d) * V + v) * Pc + ci] = c;
-            });
-        } else {
-            for (int v = 0; v < V; ++v)
-                scr[(static_cast<long long>(d) * V + v) * Pc + ci] = (d == 0 && v == 0) ? 2.0f : 0.0f;
-        }
+        pos[d] = kp.nbpos[d * Pc + ci];
+        flag[d] = pos[d] >= 0;
     }
-    auto cost_arr = [&](int d, int v) -> float { return scr[(static_cast<long long>(d) * V + v) * Pc + ci]; };
+    // cost_array[8][32] = {2.0f}: unavailable directions read as 0, element [0][0] as 2 (:957)
+    auto cost_arr = [&](int d, int v) -> float {
+        bool f = flag[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) if (k == d) f = flag[k];
+        if (!f) return (d == 0 && v == 0) ? 2.0f : 0.0f;
+        return kp.hyp_cost[(static_cast<long long>(d) * V + v) * Pc + ci];
+    };
 
     // ---- joint view selection :1146-1208
     float vsp[kMaxViews];
@@ -803,6 +899,7 @@ __global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int c
     {
         const int nbx[4] = {px, px, px - 1, px + 1};
         const int nby[4] = {py - 1, py + 1, py, py};
+#pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (flag[2 * i]) {
                 const uint32_t sv = kp.sel_cs[(nbx[i] + nby[i]) & 1][cs_index(kp, nbx[i], nby[i])];
@@ -879,17 +976,17 @@ __global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int c
         for (int i = 1; i < 8; ++i) if (final_costs[i] <= m) { m = final_costs[i]; min_idx = i; }
     }
 
-    // ---- current hypothesis :1232-1245
-    const uint32_t wmask = wave_or(temp_sel);
+    // ---- current hypothesis :1232-1245 (zero-weight views add +0: skipped)
     float4 cur_plane = kp.plane_cs[colour][ci];
     float cost_now = 0.0f;
-    for_all_views<MODEL, VB>(kp, px, py, pt, cur_plane, wmask, [&](int v, float c) {
+    for (int v = 0; v < V; ++v) {
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
+            const float c = kp.hyp_cost[(static_cast<long long>(8) * V + v) * Pc + ci];
             if (kp.geom) cost_now = fmaf(w, fmaf(0.2f, geom_cost<MODEL>(kp, v + 1, cur_plane, px, py, dc), c), cost_now);
             else cost_now = fmaf(w, c, cost_now);
         }
-    });
+    }
     cost_now /= weight_norm;
     float cur_cost = cost_now;
     uint32_t cur_sel = kp.sel_cs[colour][ci];
@@ -897,20 +994,14 @@ __global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int c
     float restricted_cost = 0.0f;
     const bool use_prior = kp.planar && kp.mask[center] > 0;
 
-    auto sel_plane = [&](int i) -> float4 {
-        float4 r = plane_at(kp, pos[0]);
+    auto sel_pos = [&](int i) -> int {
+        int r = pos[0];
 #pragma unroll
-        for (int k = 1; k < 8; ++k) if (k == i) r = plane_at(kp, pos[k]);
+        for (int k = 1; k < 8; ++k) if (k == i) r = pos[k];
         return r;
     };
     auto sel_f = [&](const float (&a)[8], int i) -> float {
         float r = a[0];
-#pragma unroll
-        for (int k = 1; k < 8; ++k) if (k == i) r = a[k];
-        return r;
-    };
-    auto sel_b = [&](const bool (&a)[8], int i) -> bool {
-        bool r = a[0];
 #pragma unroll
         for (int k = 1; k < 8; ++k) if (k == i) r = a[k];
         return r;
@@ -948,8 +1039,9 @@ __global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int c
             const float ad = det_acos(dot3n(prior, cur_plane));
             const float pr = fmaf(det_exp((-ddiff) * ddiff / two_dss), det_exp((-ad) * ad / two_ass), gamma);
             const float rc_now = det_exp((-cost_now) * cost_now / beta) * pr;
-            if (sel_b(flag, max_idx)) {
-                const float4 nb = sel_plane(max_idx);
+            const int mpos = sel_pos(max_idx);
+            if (mpos >= 0) {
+                const float4 nb = plane_at(kp, mpos);
                 const float db = depth_from_plane(nb, dc);
                 const float rmax = sel_f(rfc, max_idx);
                 if (db >= kp.depth_min && db <= kp.depth_max && rmax > rc_now) {
@@ -960,47 +1052,49 @@ __global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int c
                     cur_sel = temp_sel;
                 }
             }
-        } else if (sel_b(flag, min_idx)) {
-            const float4 nb = sel_plane(min_idx);
-            const float db = depth_from_plane(nb, dc);
-            const float fmin = sel_f(final_costs, min_idx);
-            if (db >= kp.depth_min && db <= kp.depth_max && fmin < cost_now) {
-                depth_now = db;
-                cur_plane = nb;
-                cur_cost = fmin;
+        } else {
+            const int mpos = sel_pos(min_idx);
+            if (mpos >= 0) {
+                const float4 nb = plane_at(kp, mpos);
+                const float db = depth_from_plane(nb, dc);
+                const float fmin = sel_f(final_costs, min_idx);
+                if (db >= kp.depth_min && db <= kp.depth_max && fmin < cost_now) {
+                    depth_now = db;
+                    cur_plane = nb;
+                    cur_cost = fmin;
+                }
             }
         }
     }
 
     float4 plane_now = cur_plane;                           // fix A (:1301)
-    if (!kp.planar && sel_b(flag, min_idx)) {               // :1302-1311
-        const float4 nb = sel_plane(min_idx);
-        const float db = depth_from_plane(nb, dc);
-        const float fmin = sel_f(final_costs, min_idx);
-        if (db >= kp.depth_min && db <= kp.depth_max && fmin < cost_now) {
-            depth_now = db;
-            plane_now = nb;
-            cost_now = fmin;
-            cur_sel = temp_sel;
+    if (!kp.planar) {                                       // :1302-1311
+        const int mpos = sel_pos(min_idx);
+        if (mpos >= 0) {
+            const float4 nb = plane_at(kp, mpos);
+            const float db = depth_from_plane(nb, dc);
+            const float fmin = sel_f(final_costs, min_idx);
+            if (db >= kp.depth_min && db <= kp.depth_max && fmin < cost_now) {
+                depth_now = db;
+                plane_now = nb;
+                cost_now = fmin;
+                cur_sel = temp_sel;
+            }
         }
     }
 
-    // ---- PlaneHypothesisRefinement :797-936
+    // ---- PlaneHypothesisRefinement candidates :813-874
+    uint32_t flags = use_prior ? 1u : 0u;
     if (weight_norm > 0.0f) {
+        flags |= 2u;
         const float perturbation = 0.02f;
-        const float gamma = 0.5f;
         const float depth_sigma = (kp.depth_max - kp.depth_min) / 64.0f;
-        const float two_dss = 2 * depth_sigma * depth_sigma;
         const float angle_sigma = kCudartPiF * (5.0f / 180.0f);
-        const float two_ass = 2 * angle_sigma * angle_sigma;
-        const float beta = 0.18f;
         float depth_rand;
         float4 n_rand;
-        float4 prior = make_float4(0.f, 0.f, 0.f, 0.f);
-        float dprior = 0.f;
         if (use_prior) {
-            prior = kp.prior[center];
-            dprior = depth_from_plane(prior, dc);
+            const float4 prior = kp.prior[center];
+            const float dprior = depth_from_plane(prior, dc);
             depth_rand = sample_depth_inv(rs, fmaxf(dprior - 3 * depth_sigma, kp.depth_min),
                                           fminf(dprior + 3 * depth_sigma, kp.depth_max));
             n_rand = perturbed_normal(dc, prior, rs, angle_sigma);
@@ -1019,39 +1113,122 @@ __global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int c
         }
         if (!ok) depth_perturbed = fminf(fmaxf(depth_now, kp.depth_min), kp.depth_max);
         const float4 n_pert = perturbed_normal(dc, plane_now, rs, perturbation * kCudartPiF);
-        const float d0 = depth_now;
-        const float4 p0 = plane_now;
+#pragma unroll
         for (int i = 0; i < 5; ++i) {
-            const float dep = (i == 0 || i == 2) ? depth_rand : (i == 4 ? depth_perturbed : d0);
-            float4 tp = (i == 1 || i == 2) ? n_rand : (i == 3 ? n_pert : p0);
+            const float dep = (i == 0 || i == 2) ? depth_rand : (i == 4 ? depth_perturbed : depth_now);
+            float4 tp = (i == 1 || i == 2) ? n_rand : (i == 3 ? n_pert : plane_now);
             tp.w = dist_to_origin(dc, dep, tp);
-            float temp_cost = 0.0f;
-            for_all_views<MODEL, VB>(kp, px, py, pt, tp, wmask, [&](int v, float c) {
-                const float w = vw_get(vwp, v);
-                if (w > 0.0f) {
-                    if (kp.geom) temp_cost = fmaf(w, fmaf(0.1f, geom_cost<MODEL>(kp, v + 1, tp, px, py, dc), c), temp_cost);
-                    else temp_cost = fmaf(w, c, temp_cost);
-                }
-            });
-            temp_cost /= weight_norm;
+            kp.cand[i * Pc + ci] = tp;
+            kp.cand_dep[i * Pc + ci] = dep;
+        }
+    }
+    PixState st;
+    st.plane_now = plane_now;
+    st.cur_plane = cur_plane;
+    st.vw = make_uint4(vwp[0], vwp[1], vwp[2], vwp[3]);
+    st.cost_now = cost_now;
+    st.depth_now = depth_now;
+    st.cur_cost = cur_cost;
+    st.restricted_cost = restricted_cost;
+    st.cur_sel = cur_sel;
+    st.flags = flags;
+    st.weight_norm = weight_norm;
+    st.pad = 0u;
+    kp.pst[ci] = st;
+    kp.rng_cs[colour][ci] = rs.n;
+}
+
+// Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
+template <int MODEL, int VB>
+__global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int colour) {
+    __shared__ float lw[kRefPix * 64];
+    __shared__ float lr[kRefPix * 64];
+    __shared__ float lsum[kRefPix * 3];
+    const int t = threadIdx.x;
+    const int lp = t / kRefLanes, h = t - lp * kRefLanes;
+    const long long q = static_cast<long long>(blockIdx.x) * kRefPix + lp;
+    int px = 0, py = 0;
+    bool valid = t < kRefPix * kRefLanes && colour_pixel(kp, colour, q, px, py);
+    const long long Pc = kp.Pc;
+    const long long ci = valid ? static_cast<long long>(py) * kp.Wh + (px >> 1) : 0;
+    uint4 vw = make_uint4(0u, 0u, 0u, 0u);
+    float weight_norm = 0.0f;
+    if (valid) {
+        const PixState& st = kp.pst[ci];
+        valid = (st.flags & 2u) != 0u;
+        vw = st.vw;
+        weight_norm = st.weight_norm;
+    }
+    coop_weights<MODEL>(kp, valid, px, py, lp, h, kRefLanes, lw, lr, lsum);
+    if (!valid) return;
+    const float4 dc = ray_at<MODEL>(kp, px, py);
+    const float4 tp = kp.cand[h * Pc + ci];
+    const float depth_before = depth_from_plane(tp, dc);
+    if (depth_before < kp.depth_min || depth_before > kp.depth_max || depth_before >= 1e6f) return;  // :903-906
+    const uint32_t vwp[4] = {vw.x, vw.y, vw.z, vw.w};
+    uint32_t mask = 0u;
+    for (int v = 0; v < kp.V; ++v) if (vw_get(vwp, v) > 0.0f) mask |= 1u << v;
+    const Patch pt = patch_from_lds<MODEL>(kp, px, py, lp, lw, lsum);
+    float temp_cost = 0.0f;
+    for_all_views<MODEL, VB>(kp, px, py, pt, tp, wave_or(mask, kp.V), [&](int v, float c) {
+        const float w = vw_get(vwp, v);
+        if (w > 0.0f) {
+            if (kp.geom) temp_cost = fmaf(w, fmaf(0.1f, geom_cost<MODEL>(kp, v + 1, tp, px, py, dc), c), temp_cost);
+            else temp_cost = fmaf(w, c, temp_cost);
+        }
+    });
+    kp.cand_cost[h * Pc + ci] = temp_cost / weight_norm;
+}
+
+// Refinement acceptance in candidate order (ACMMP.cu:902-935), hierarchy gate (:1315-1324), store.
+template <int MODEL>
+__global__ __launch_bounds__(256) void k_finish(const KParams kp, const int colour, const SweepOut out) {
+    const long long q = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+    int px = 0, py = 0;
+    if (!colour_pixel(kp, colour, q, px, py)) return;
+    const long long Pc = kp.Pc;
+    const long long ci = static_cast<long long>(py) * kp.Wh + (px >> 1);
+    const long long center = static_cast<long long>(py) * kp.W + px;
+    const float4 dc = ray_at<MODEL>(kp, px, py);
+    const PixState st = kp.pst[ci];
+    float4 plane_now = st.plane_now;
+    float cost_now = st.cost_now;
+    float restricted_cost = st.restricted_cost;
+    if (st.flags & 2u) {
+        const bool use_prior = (st.flags & 1u) != 0u;
+        const float gamma = 0.5f;
+        const float depth_sigma = (kp.depth_max - kp.depth_min) / 64.0f;
+        const float two_dss = 2 * depth_sigma * depth_sigma;
+        const float angle_sigma = kCudartPiF * (5.0f / 180.0f);
+        const float two_ass = 2 * angle_sigma * angle_sigma;
+        const float beta = 0.18f;
+        float4 prior = make_float4(0.f, 0.f, 0.f, 0.f);
+        float dprior = 0.f;
+        if (use_prior) {
+            prior = kp.prior[center];
+            dprior = depth_from_plane(prior, dc);
+        }
+        for (int i = 0; i < 5; ++i) {
+            const float4 tp = kp.cand[i * Pc + ci];
             const float depth_before = depth_from_plane(tp, dc);
             if (depth_before < kp.depth_min || depth_before > kp.depth_max || depth_before >= 1e6f) continue;
+            const float temp_cost = kp.cand_cost[i * Pc + ci];
             if (use_prior) {
-                const float ddiff = dep - dprior;
+                const float ddiff = kp.cand_dep[i * Pc + ci] - dprior;
                 const float ac = fminf(fmaxf(dot3n(prior, tp), -1.0f), 1.0f);
                 const float ad = det_acos(ac);
                 const float pr = fmaf(det_exp((-ddiff) * ddiff / two_dss), det_exp((-ad) * ad / two_ass), gamma);
                 const float rtc = det_exp((-temp_cost) * temp_cost / beta) * pr;
-                if (rtc > restricted_cost) {
-                    depth_now = depth_before; plane_now = tp; cost_now = temp_cost; restricted_cost = rtc;
-                }
+                if (rtc > restricted_cost) { plane_now = tp; cost_now = temp_cost; restricted_cost = rtc; }
             } else if (temp_cost < cost_now) {
-                depth_now = depth_before; plane_now = tp; cost_now = temp_cost;
+                plane_now = tp;
+                cost_now = temp_cost;
             }
         }
     }
-
-    if (kp.hier) {                                          // :1315-1324
+    float4 cur_plane = st.cur_plane;
+    float cur_cost = st.cur_cost;
+    if (kp.hier) {
         if (cost_now < kp.pre_rm[center] - 0.1f) { cur_cost = cost_now; cur_plane = plane_now; }
     } else {
         cur_cost = cost_now;
@@ -1059,8 +1236,7 @@ __global__ __launch_bounds__(256) void k_propagate(const KParams kp, const int c
     }
     out.plane[ci] = cur_plane;
     out.cost[ci] = cur_cost;
-    kp.sel_cs[colour][ci] = cur_sel;
-    kp.rng_cs[colour][ci] = rs.n;
+    kp.sel_cs[colour][ci] = st.cur_sel;
 }
 
 // ------------------------------------------------------------------ kernels: post
@@ -1239,9 +1415,13 @@ hipError_t launch_init(const KParams& kp, hipStream_t s) {
 }
 
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s) {
-    dim3 blk(64, 4), grd(cdiv(kp.Wh, 64), cdiv(kp.rows, 4));
-    const size_t lds = sizeof(float) * kp.S * 256;
-    ACMMP_DISPATCH(kp.model, kp.V, (k_propagate<M, VBC><<<grd, blk, lds, s>>>(kp, colour, iter, out)));
+    const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
+    ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC><<<cdiv(npix, kNbPix), 256, 0, s>>>(kp, colour)));
+    if (kp.model == kSphere) k_select<kSphere><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter);
+    else k_select<kPinhole><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter);
+    ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC><<<cdiv(npix, kRefPix), 256, 0, s>>>(kp, colour)));
+    if (kp.model == kSphere) k_finish<kSphere><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, out);
+    else k_finish<kPinhole><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, out);
     return hipGetLastError();
 }
 
