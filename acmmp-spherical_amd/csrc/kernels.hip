@@ -119,9 +119,9 @@ __device__ __forceinline__ float3 world_point_ray(const DevCam& c, int x, int y,
     }
 }
 
-// ProjectonCamera_cu, ACMMP.cu:602-644
-template <int MODEL>
-__device__ __forceinline__ void project(const DevCam& c, float3 P, float& ox, float& oy, float& depth) {
+// ProjectonCamera_cu, ACMMP.cu:602-644 (Cam: DevCam in any address space)
+template <int MODEL, typename Cam>
+__device__ __forceinline__ void project(Cam& c, float3 P, float& ox, float& oy, float& depth) {
     const float tx = dot3(c.R[0], c.R[1], c.R[2], P.x, P.y, P.z) + c.t[0];
     const float ty = dot3(c.R[3], c.R[4], c.R[5], P.x, P.y, P.z) + c.t[1];
     const float tz = dot3(c.R[6], c.R[7], c.R[8], P.x, P.y, P.z) + c.t[2];
@@ -198,13 +198,16 @@ __device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_read
 
 // ------------------------------------------------------------------ NCC over a chunk of views
 
-// Per-pixel patch context: the lane's bilateral weights live in LDS (`lw[s * stride]`),
-// ACMMP.cu:436-486; SPHERE's weight sums are hypothesis- and view-independent.
+// Per-pixel patch, staged in LDS once per launch: for every sample s of the 6x6 stride-2 window
+// (ACMMP.cu:450-451) the reference ray (PixelToDir of the sample pixel), the bilateral weight
+// w_s (ACMMP.cu:398-403, 482-486) and the reference texel.  SPHERE's weight sums are
+// hypothesis- and view-independent (no sample is ever skipped there).
 struct Patch {
-    const float* lw;
+    const float4* rw;               // [s * stride] = (ray.x, ray.y, ray.z, w); null when not staged
+    const float* rr;                // [s * stride] = reference texel
     int stride;
     float center;                   // reference texel at the pixel
-    float sbw, sref, srr;           // SPHERE: sum_bw, sum_ref, sum_ref_ref over all samples
+    float sbw, sref, srr;
 };
 
 typedef float float2u __attribute__((ext_vector_type(2), aligned(4)));
@@ -225,42 +228,119 @@ __device__ __forceinline__ float bilinear_pair(const float* img, int pitch, int 
     return fmaf(b, r1 - r0, r0);
 }
 
-// Fill the lane's LDS weights: w_s = exp(spatial_s - |ref_s - center| / (2 sigma_c^2)).
+// Sample s = (i, j) of pixel (px, py): ray, bilateral weight and reference texel.
 template <int MODEL>
-__device__ __forceinline__ Patch make_patch(const KParams& kp, int px, int py, float* lw, int stride) {
+__device__ __forceinline__ float4 patch_sample(const KParams& kp, int px, int py, int s, int i, int j, float center,
+                                               float& r) {
     const DevCam& rc = kp.cams[0];
-    const float* ref = kp.img + rc.img_off;
-    Patch pt;
-    pt.lw = lw;
-    pt.stride = stride;
-    pt.center = texel_padded(ref, rc.img_pitch, rc.W, rc.H, px, py);
+    r = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px + i, py + j);
+    const float sp = kp.spatial[(MODEL == kSphere ? static_cast<long long>(py) * kp.S : 0) + s];
+    const float w = det_exp(sp - fabsf(r - center) / kp.color_den);
+    const float4 d = ray_at<MODEL>(kp, px + i, py + j);
+    return make_float4(d.x, d.y, d.z, w);
+}
+
+// Stage sample s of pixel (px, py) into its LDS slot.
+template <int MODEL>
+__device__ __forceinline__ void stage_sample(const KParams& kp, int px, int py, int s, float center, float4* rw,
+                                             float* rr) {
+    const int i = -kp.R + (s / kp.nside) * kp.inc, j = -kp.R + (s % kp.nside) * kp.inc;
+    float r;
+    *rw = patch_sample<MODEL>(kp, px, py, s, i, j, center, r);
+    *rr = r;
+}
+
+template <int MODEL>
+__device__ __forceinline__ void patch_sums(const KParams& kp, Patch& pt, int px = 0, int py = 0) {
     pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f;
-    const float* sp = kp.spatial + (MODEL == kSphere ? static_cast<long long>(py) * kp.S : 0);
-    int s = 0;
-    for (int i = -kp.R; i <= kp.R; i += kp.inc) {
-        for (int j = -kp.R; j <= kp.R; j += kp.inc, ++s) {
-            const float r = texel_padded(ref, rc.img_pitch, rc.W, rc.H, px + i, py + j);
-            const float w = det_exp(sp[s] - fabsf(r - pt.center) / kp.color_den);
-            lw[s * stride] = w;
-            if (MODEL == kSphere) {
-                pt.sbw += w;
-                pt.sref = fmaf(w, r, pt.sref);
-                pt.srr = fmaf(w * r, r, pt.srr);
+    if (MODEL == kSphere) {
+        for (int s = 0; s < kp.S; ++s) {
+            float w, r;
+            if (pt.rw) {
+                w = pt.rw[s * pt.stride].w;
+                r = pt.rr[s * pt.stride];
+            } else {
+                w = patch_sample<MODEL>(kp, px, py, s, -kp.R + (s / kp.nside) * kp.inc,
+                                        -kp.R + (s % kp.nside) * kp.inc, pt.center, r).w;
             }
+            pt.sbw += w;
+            pt.sref = fmaf(w, r, pt.sref);
+            pt.srr = fmaf(w * r, r, pt.srr);
         }
     }
+}
+
+// Unstaged patch of one lane's pixel: samples are recomputed inside the NCC loop (init / debug
+// kernels, which evaluate one or two hypotheses per pixel).
+template <int MODEL>
+__device__ __forceinline__ Patch make_patch(const KParams& kp, int px, int py) {
+    const DevCam& rc = kp.cams[0];
+    Patch pt;
+    pt.rw = nullptr; pt.rr = nullptr; pt.stride = 0;
+    pt.center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
+    patch_sums<MODEL>(kp, pt, px, py);
     return pt;
+}
+
+// Projection parameters of one source view, loaded once per chunk (wave-uniform -> SGPRs).
+struct ProjCam {
+    float R[9], t[3], K[6];
+    float Wf, Hf, invW, cx, cy;
+    int W, H, pitch;
+    const float* img;
+};
+
+__device__ __forceinline__ ProjCam load_projcam(const KParams& kp, int view) {
+    const DevCam& c = kp.cams[uniform_int(view)];
+    ProjCam p;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) p.R[k] = c.R[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) p.t[k] = c.t[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) p.K[k] = c.K[k];
+    p.Wf = c.Wf; p.Hf = c.Hf; p.invW = c.invW; p.cx = c.cx; p.cy = c.cy;
+    p.W = c.W; p.H = c.H; p.pitch = c.img_pitch;
+    p.img = kp.img + c.img_off;
+    return p;
+}
+
+// ProjectonCamera_cu (ACMMP.cu:602-644) on a ProjCam; identical arithmetic to project<MODEL>.
+template <int MODEL>
+__device__ __forceinline__ void project_pc(const ProjCam& c, float3 P, float& ox, float& oy) {
+    const float tx = dot3(c.R[0], c.R[1], c.R[2], P.x, P.y, P.z) + c.t[0];
+    const float ty = dot3(c.R[3], c.R[4], c.R[5], P.x, P.y, P.z) + c.t[1];
+    const float tz = dot3(c.R[6], c.R[7], c.R[8], P.x, P.y, P.z) + c.t[2];
+    if (MODEL == kSphere) {
+        const float d = sqrtf(dot3(tx, ty, tz, tx, ty, tz));
+        const float neg_lat = det_asin(ty / d);
+        const float lon = det_atan2(tx, tz);
+        ox = fmaf(lon * kInv2Pi, c.Wf, c.cx);
+        oy = fmaf(neg_lat * kInvPi, c.Hf, c.cy);
+        if (d < 1e-6f) { ox = c.cx; oy = c.cy; }
+    } else {
+        const float inv = 1.0f / tz;
+        ox = dot3(c.K[0], c.K[1], c.K[2], tx, ty, tz) * inv;
+        oy = dot3(c.K[3], c.K[4], c.K[5], tx, ty, tz) * inv;
+    }
 }
 
 // ComputeBilateralNCC (ACMMP.cu:405-516) of plane `ph` at pixel (px, py) against the
 // source views vlist[0..nv) (wave-uniform camera indices 1..N-1), sample-outer.
-template <int MODEL, int VB>
+template <int MODEL, int VB, bool STAGED>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv, float (&cost)[VB]) {
     const DevCam& rc = kp.cams[0];
-    const float* ref = kp.img + rc.img_off;
     float sbw[VB], sref[VB], srr[VB], ssrc[VB], sss[VB], srs[VB];
     bool cval[VB];
+    int cv[VB];
+#pragma unroll
+    for (int v = 0; v < VB; ++v) cv[v] = uniform_int(v < nv ? vlist[v] : vlist[0]);
+    // camera table is read-only for the whole launch: view it through the constant address space so
+    // every field becomes a scalar (SMEM) load of a wave-uniform address
+    typedef const __attribute__((address_space(4))) DevCam ConstCam;
+    ConstCam* ccams = (ConstCam*)(kp.cams);
+#define PCV(v) ccams[cv[v]]
     const float4 dc = ray_at<MODEL>(kp, px, py);
     const float3 Pc3 = world_point_ray<MODEL>(rc, px, py, depth_from_plane(ph, dc), dc);
 #pragma unroll
@@ -269,26 +349,30 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
         ssrc[v] = 0.f; sss[v] = 0.f; srs[v] = 0.f;
         cval[v] = true;
         if (MODEL == kPinhole && v < nv) {
-            const DevCam& c = kp.cams[vlist[v]];
             float ox, oy, od;
-            project<MODEL>(c, Pc3, ox, oy, od);
-            cval[v] = !(ox < 0.0f || ox >= c.Wf || oy < 0.0f || oy >= c.Hf);
+            project<MODEL>(PCV(v), Pc3, ox, oy, od);
+            cval[v] = !(ox < 0.0f || ox >= PCV(v).Wf || oy < 0.0f || oy >= PCV(v).Hf);
         }
     }
     const int R = kp.R, inc = kp.inc;
     int s = 0;
     for (int i = -R; i <= R; i += inc) {
         for (int j = -R; j <= R; j += inc, ++s) {
-            const int rx = px + i, ry = py + j;
-            const float4 d = ray_at<MODEL>(kp, rx, ry);
-            const float3 P = world_point_ray<MODEL>(rc, rx, ry, depth_from_plane(ph, d), d);
-            const float w = pt.lw[s * pt.stride];
-            const float r = texel_padded(ref, rc.img_pitch, rc.W, rc.H, rx, ry);
+            float r;
+            float4 rw;
+            if (STAGED) {
+                rw = pt.rw[s * pt.stride];
+                r = pt.rr[s * pt.stride];
+            } else {
+                rw = patch_sample<MODEL>(kp, px, py, s, i, j, pt.center, r);
+            }
+            const float w = rw.w;
+            const float3 P = world_point_ray<MODEL>(rc, px + i, py + j, depth_from_plane(ph, rw), rw);
             const float wr = w * r;
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
                 if (v < nv) {
-                    const DevCam& c = kp.cams[vlist[v]];
+                    ConstCam& c = PCV(v);
                     float sx, sy, sd;
                     project<MODEL>(c, P, sx, sy, sd);
                     bool ok = true;
@@ -298,8 +382,8 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                     } else {
                         ok = !(sx < 0.0f || sx >= c.Wf || sy < 0.0f || sy >= c.Hf);
                     }
+                    const float sp = bilinear_pair(kp.img + c.img_off, c.img_pitch, c.W, c.H, sx, sy);
                     if (ok) {
-                        const float sp = bilinear_pair(kp.img + c.img_off, c.img_pitch, c.W, c.H, sx, sy);
                         if (MODEL == kPinhole) {
                             sbw[v] += w;
                             sref[v] = fmaf(w, r, sref[v]);
@@ -331,6 +415,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
         }
         cost[v] = out;
     }
+#undef PCV
 }
 
 // ComputeGeomConsistencyCost, ACMMP.cu:646-671 (sv = source camera index 1..N-1)
@@ -417,7 +502,7 @@ __device__ __forceinline__ float4 perturbed_normal(float4 v, float4 n, Rng& rs, 
 // ------------------------------------------------------------------ cost-vector helpers
 
 // Evaluate all source views of plane `ph` and hand each cost to f(view0, cost) in view order.
-template <int MODEL, int VB, typename F>
+template <int MODEL, int VB, bool STAGED, typename F>
 __device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                               uint32_t wave_mask, F&& f) {
     int v = 0;
@@ -439,7 +524,7 @@ __device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py,
         }
         if (nv == 0) break;
         float cost[VB];
-        ncc_chunk<MODEL, VB>(kp, px, py, pt, ph, vlist, nv, cost);
+        ncc_chunk<MODEL, VB, STAGED>(kp, px, py, pt, ph, vlist, nv, cost);
 #pragma unroll
         for (int k = 0; k < VB; ++k)
             if (k < nv) f(vlist[k] - 1, cost[k]);
@@ -532,7 +617,7 @@ __device__ float initial_cost(const KParams& kp, int px, int py, const Patch& pt
     float cv[kMaxViews], cvc[kMaxViews];
     int nvalid = 0;
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
-    for_all_views<MODEL, VB>(kp, px, py, pt, ph, all, [&](int v, float c) {
+    for_all_views<MODEL, VB, false>(kp, px, py, pt, ph, all, [&](int v, float c) {
         cv[v] = c;
         cvc[v] = c;
         if (c < 2.0f) nvalid++;
@@ -574,9 +659,7 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
     const long long center = static_cast<long long>(y) * kp.W + x;
     const int colour = (x + y) & 1;
     const long long ci = cs_index(kp, x, y);
-    extern __shared__ float lds_w[];
-    const int tid = threadIdx.y * blockDim.x + threadIdx.x;
-    const Patch pt = make_patch<MODEL>(kp, x, y, lds_w + tid, blockDim.x * blockDim.y);
+    const Patch pt = make_patch<MODEL>(kp, x, y);
     Rng rs;
     rs.init(kp.seed_lo, kp.seed_hi, static_cast<uint32_t>(center), 0u);
     const float4 dc = ray_at<MODEL>(kp, x, y);
@@ -783,48 +866,29 @@ __device__ __forceinline__ bool colour_pixel(const KParams& kp, int colour, long
     return py < kp.rows && px < kp.W;
 }
 
-// Cooperative LDS weights for the block's pixels: lane `h` of `nh` lanes of pixel slot `lp`
-// computes samples h, h+nh, ... (ACMMP.cu:436-486); SPHERE sums by the first lane of each pixel.
+// Cooperative staging of the block's pixels: lane `h` of the `nh` lanes of pixel slot `lp`
+// stages samples h, h+nh, ...; the first lane of each pixel then forms the SPHERE sums.
 template <int MODEL>
-__device__ __forceinline__ void coop_weights(const KParams& kp, bool valid, int px, int py, int lp, int h, int nh,
-                                             float* lw, float* lr, float* lsum) {
+__device__ __forceinline__ Patch coop_patch(const KParams& kp, bool valid, int px, int py, int lp, int h, int nh,
+                                            float4* lrw, float* lrr, float* lsum) {
+    float4* rw = lrw + lp * kp.S;
+    float* rr = lrr + lp * kp.S;
     if (valid) {
         const DevCam& rc = kp.cams[0];
-        const float* ref = kp.img + rc.img_off;
-        const float center = texel_padded(ref, rc.img_pitch, rc.W, rc.H, px, py);
-        const float* sp = kp.spatial + (MODEL == kSphere ? static_cast<long long>(py) * kp.S : 0);
-        for (int s = h; s < kp.S; s += nh) {
-            const int i = -kp.R + (s / kp.nside) * kp.inc, j = -kp.R + (s % kp.nside) * kp.inc;
-            const float r = texel_padded(ref, rc.img_pitch, rc.W, rc.H, px + i, py + j);
-            lw[lp * kp.S + s] = det_exp(sp[s] - fabsf(r - center) / kp.color_den);
-            lr[lp * kp.S + s] = r;
-        }
+        const float center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
+        for (int s = h; s < kp.S; s += nh) stage_sample<MODEL>(kp, px, py, s, center, rw + s, rr + s);
     }
     __syncthreads();
-    if (MODEL == kSphere && valid && h == 0) {
-        float sbw = 0.f, sref = 0.f, srr = 0.f;
-        for (int s = 0; s < kp.S; ++s) {
-            const float w = lw[lp * kp.S + s], r = lr[lp * kp.S + s];
-            sbw += w;
-            sref = fmaf(w, r, sref);
-            srr = fmaf(w * r, r, srr);
-        }
-        lsum[lp * 3 + 0] = sbw; lsum[lp * 3 + 1] = sref; lsum[lp * 3 + 2] = srr;
-    }
-    __syncthreads();
-}
-
-template <int MODEL>
-__device__ __forceinline__ Patch patch_from_lds(const KParams& kp, int px, int py, int lp, const float* lw,
-                                                const float* lsum) {
-    const DevCam& rc = kp.cams[0];
     Patch pt;
-    pt.lw = lw + lp * kp.S;
-    pt.stride = 1;
-    pt.center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
-    pt.sbw = MODEL == kSphere ? lsum[lp * 3 + 0] : 0.f;
-    pt.sref = MODEL == kSphere ? lsum[lp * 3 + 1] : 0.f;
-    pt.srr = MODEL == kSphere ? lsum[lp * 3 + 2] : 0.f;
+    pt.rw = rw; pt.rr = rr; pt.stride = 1;
+    pt.center = 0.f;
+    if (MODEL == kSphere && valid && h == 0) {
+        patch_sums<MODEL>(kp, pt);
+        lsum[lp * 3 + 0] = pt.sbw; lsum[lp * 3 + 1] = pt.sref; lsum[lp * 3 + 2] = pt.srr;
+    }
+    __syncthreads();
+    pt.sbw = lsum[lp * 3 + 0]; pt.sref = lsum[lp * 3 + 1]; pt.srr = lsum[lp * 3 + 2];
+    if (MODEL != kSphere) { pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f; }
     return pt;
 }
 
@@ -835,15 +899,16 @@ constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 la
 
 template <int MODEL, int VB>
 __global__ __launch_bounds__(256) void k_eval_nb(const KParams kp, const int colour) {
-    __shared__ float lw[kNbPix * 64];
-    __shared__ float lr[kNbPix * 64];
-    __shared__ float lsum[kNbPix * 3];
+    extern __shared__ float4 lds4[];
+    float4* lrw = lds4;
+    float* lrr = reinterpret_cast<float*>(lds4 + kNbPix * kp.S);
+    float* lsum = lrr + kNbPix * kp.S;
     const int t = threadIdx.x;
     const int lp = t / kNbLanes, h = t - lp * kNbLanes;
     const long long q = static_cast<long long>(blockIdx.x) * kNbPix + lp;
     int px = 0, py = 0;
     const bool valid = t < kNbPix * kNbLanes && colour_pixel(kp, colour, q, px, py);
-    coop_weights<MODEL>(kp, valid, px, py, lp, h, kNbLanes, lw, lr, lsum);
+    const Patch pt = coop_patch<MODEL>(kp, valid, px, py, lp, h, kNbLanes, lrw, lrr, lsum);
     if (!valid) return;
     const long long Pc = kp.Pc;
     const long long ci = static_cast<long long>(py) * kp.Wh + (px >> 1);
@@ -856,10 +921,9 @@ __global__ __launch_bounds__(256) void k_eval_nb(const KParams kp, const int col
     } else {
         ph = kp.plane_cs[colour][ci];
     }
-    const Patch pt = patch_from_lds<MODEL>(kp, px, py, lp, lw, lsum);
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
-    for_all_views<MODEL, VB>(kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
+    for_all_views<MODEL, VB, true>(kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
 }
 
 // Joint view selection, aggregation, acceptance and refinement candidates (ACMMP.cu:1146-1311,
@@ -1141,9 +1205,10 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
 template <int MODEL, int VB>
 __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int colour) {
-    __shared__ float lw[kRefPix * 64];
-    __shared__ float lr[kRefPix * 64];
-    __shared__ float lsum[kRefPix * 3];
+    extern __shared__ float4 lds4[];
+    float4* lrw = lds4;
+    float* lrr = reinterpret_cast<float*>(lds4 + kRefPix * kp.S);
+    float* lsum = lrr + kRefPix * kp.S;
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
     const long long q = static_cast<long long>(blockIdx.x) * kRefPix + lp;
@@ -1159,7 +1224,7 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
         vw = st.vw;
         weight_norm = st.weight_norm;
     }
-    coop_weights<MODEL>(kp, valid, px, py, lp, h, kRefLanes, lw, lr, lsum);
+    const Patch pt = coop_patch<MODEL>(kp, valid, px, py, lp, h, kRefLanes, lrw, lrr, lsum);
     if (!valid) return;
     const float4 dc = ray_at<MODEL>(kp, px, py);
     const float4 tp = kp.cand[h * Pc + ci];
@@ -1168,9 +1233,8 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
     const uint32_t vwp[4] = {vw.x, vw.y, vw.z, vw.w};
     uint32_t mask = 0u;
     for (int v = 0; v < kp.V; ++v) if (vw_get(vwp, v) > 0.0f) mask |= 1u << v;
-    const Patch pt = patch_from_lds<MODEL>(kp, px, py, lp, lw, lsum);
     float temp_cost = 0.0f;
-    for_all_views<MODEL, VB>(kp, px, py, pt, tp, wave_or(mask, kp.V), [&](int v, float c) {
+    for_all_views<MODEL, VB, true>(kp, px, py, pt, tp, wave_or(mask, kp.V), [&](int v, float c) {
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
             if (kp.geom) temp_cost = fmaf(w, fmaf(0.1f, geom_cost<MODEL>(kp, v + 1, tp, px, py, dc), c), temp_cost);
@@ -1345,11 +1409,10 @@ __global__ void k_debug(const KParams kp, int which, int n, const int* __restric
     const float4 ph = planes[q];
     const int colour = (x + y) & 1;
     (void)colour;
-    extern __shared__ float lds_w[];
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     if (which == 0) {
-        const Patch pt = make_patch<MODEL>(kp, x, y, lds_w + threadIdx.x, blockDim.x);
-        for_all_views<MODEL, VB>(kp, x, y, pt, ph, all,
+        const Patch pt = make_patch<MODEL>(kp, x, y);
+        for_all_views<MODEL, VB, false>(kp, x, y, pt, ph, all,
                                  [&](int v, float c) { out[static_cast<long long>(q) * kp.V + v] = c; });
     } else {
         const float4 dc = ray_at<MODEL>(kp, x, y);
@@ -1409,17 +1472,18 @@ static inline int pick_vb(int V) { return V <= 1 ? 1 : (V <= 2 ? 2 : (V <= 4 ? 4
 
 hipError_t launch_init(const KParams& kp, hipStream_t s) {
     dim3 blk(16, 16), grd(cdiv(kp.W, 16), cdiv(kp.H, 16));
-    const size_t lds = sizeof(float) * kp.S * 256;
-    ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC><<<grd, blk, lds, s>>>(kp)));
+    ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC><<<grd, blk, 0, s>>>(kp)));
     return hipGetLastError();
 }
 
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s) {
     const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
-    ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC><<<cdiv(npix, kNbPix), 256, 0, s>>>(kp, colour)));
+    const size_t lds_nb = (sizeof(float4) + sizeof(float)) * kNbPix * kp.S + sizeof(float) * 3 * kNbPix;
+    const size_t lds_ref = (sizeof(float4) + sizeof(float)) * kRefPix * kp.S + sizeof(float) * 3 * kRefPix;
+    ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC><<<cdiv(npix, kNbPix), 256, lds_nb, s>>>(kp, colour)));
     if (kp.model == kSphere) k_select<kSphere><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter);
     else k_select<kPinhole><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter);
-    ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC><<<cdiv(npix, kRefPix), 256, 0, s>>>(kp, colour)));
+    ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC><<<cdiv(npix, kRefPix), 256, lds_ref, s>>>(kp, colour)));
     if (kp.model == kSphere) k_finish<kSphere><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, out);
     else k_finish<kPinhole><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, out);
     return hipGetLastError();
@@ -1449,8 +1513,7 @@ hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int s
 hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,
                         float* out, hipStream_t s) {
     dim3 blk(64), grd(cdiv(n, 64));
-    const size_t lds = sizeof(float) * kp.S * 64;
-    ACMMP_DISPATCH(kp.model, kp.V, (k_debug<M, VBC><<<grd, blk, lds, s>>>(kp, which, n, px, py, planes, out)));
+    ACMMP_DISPATCH(kp.model, kp.V, (k_debug<M, VBC><<<grd, blk, 0, s>>>(kp, which, n, px, py, planes, out)));
     return hipGetLastError();
 }
 
