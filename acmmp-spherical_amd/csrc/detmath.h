@@ -32,12 +32,12 @@ ACMMP_HD float bits_to_f(uint32_t u) { return __builtin_bit_cast(float, u); }
 ACMMP_HD uint32_t f_to_bits(float f) { return __builtin_bit_cast(uint32_t, f); }
 ACMMP_HD float pow2i(int n) { return bits_to_f(static_cast<uint32_t>(n + 127) << 23); }
 
-// float -> int32: truncate toward zero, saturate, NaN -> 0 (v_cvt_i32_f32 semantics)
+// float -> int32: truncate toward zero, saturate, NaN -> 0 (v_cvt_i32_f32 semantics), branch-free:
+// the clamp bounds are exact binary32 values inside the int32 range.
 ACMMP_HD int f2i_sat(float x) {
-    if (x != x) return 0;
-    if (x >= 2147483648.0f) return 2147483647;
-    if (x < -2147483648.0f) return -2147483647 - 1;
-    return static_cast<int>(x);
+    int r = static_cast<int>(fminf(fmaxf(x, -2147483648.0f), 2147483520.0f));
+    r = x >= 2147483648.0f ? 2147483647 : r;
+    return x != x ? 0 : r;
 }
 
 ACMMP_HD float det_exp(float x) {
@@ -96,10 +96,10 @@ ACMMP_HD float det_asin_core(float x, float z) {
     return fmaf(x * z, p, x);
 }
 
+// asin with one data-dependent branch (|x| <= 0.5).  |x| > 1 and NaN need no test: they take
+// the second path, where sqrt of a negative / NaN argument yields the NaN.
 ACMMP_HD float det_asin(float x) {
-    if (x != x) return x;
     const float a = fabsf(x);
-    if (a > 1.0f) return __builtin_nanf("");
     float r;
     if (a <= 0.5f) {
         r = det_asin_core(a, a * a);
@@ -126,20 +126,24 @@ ACMMP_HD float det_acos(float x) {
     return (kPio2Hi - r) + kPio2Lo;
 }
 
-ACMMP_HD float det_atan2(float y, float x) {
+// C99 special cases of atan2: NaN, zero and infinite arguments.
+ACMMP_HD float det_atan2_special(float y, float x) {
     if (x != x || y != y) return x + y;
     const float ax = fabsf(x), ay = fabsf(y);
     const bool xneg = (f_to_bits(x) >> 31) != 0;
     if (ay == 0.0f) return xneg ? copysignf(kPiHi, y) : copysignf(0.0f, y);
     if (ax == 0.0f) return copysignf(kPio2Hi, y);
-    const bool ix = ax == __builtin_inff(), iy = ay == __builtin_inff();
-    if (ix || iy) {
-        float r;
-        if (ix && iy) r = xneg ? 2.35619449615478516f : 0.785398185253143311f;
-        else if (ix) r = xneg ? kPiHi : 0.0f;
-        else r = kPio2Hi;
-        return copysignf(r, y);
-    }
+    float r;
+    if (ax == __builtin_inff() && ay == __builtin_inff()) r = xneg ? 2.35619449615478516f : 0.785398185253143311f;
+    else if (ax == __builtin_inff()) r = xneg ? kPiHi : 0.0f;
+    else r = kPio2Hi;
+    return copysignf(r, y);
+}
+
+// atan2: branch-free main path for finite non-zero arguments; the rare special arguments are
+// re-evaluated by det_atan2_special in a branch that a wave only takes when one of its lanes needs it.
+ACMMP_HD float det_atan2(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
     const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
     const float t = mn / mx;
     const float z = t * t;
@@ -155,9 +159,14 @@ ACMMP_HD float det_atan2(float y, float x) {
     p = fmaf(p, z, 0.199999913573265076f);
     p = fmaf(p, z, -0.333333343267440796f);
     float r = fmaf(t * z, p, t);
-    if (ay > ax) r = (kPio2Hi - r) + kPio2Lo;
-    if (xneg) r = (kPiHi - r) + kPiLo;
-    return copysignf(r, y);
+    const float rs = (kPio2Hi - r) + kPio2Lo;
+    r = ay > ax ? rs : r;
+    const float rn = (kPiHi - r) + kPiLo;
+    r = (f_to_bits(x) >> 31) ? rn : r;
+    r = copysignf(r, y);
+    const bool regular = ay != 0.0f && ax != 0.0f && ax < __builtin_inff() && ay < __builtin_inff();
+    if (!regular) r = det_atan2_special(y, x);
+    return r;
 }
 
 ACMMP_HD float det_rsqrt(float x) { return 1.0f / sqrtf(x); }

@@ -128,11 +128,11 @@ __device__ __forceinline__ void project(Cam& c, float3 P, float& ox, float& oy, 
     if (MODEL == kSphere) {
         const float d = sqrtf(dot3(tx, ty, tz, tx, ty, tz));
         depth = d;
-        if (d < 1e-6f) { ox = c.cx; oy = c.cy; return; }
         const float neg_lat = det_asin(ty / d);
         const float lon = det_atan2(tx, tz);
         ox = fmaf(lon * kInv2Pi, c.Wf, c.cx);
         oy = fmaf(neg_lat * kInvPi, c.Hf, c.cy);
+        if (d < 1e-6f) { ox = c.cx; oy = c.cy; }        // (:618-622) selected, not branched around
     } else {
         depth = tz;
         const float inv = 1.0f / tz;
