@@ -25,7 +25,7 @@ EXPORTS = [
     "acmmp_set_params", "acmmp_upload_views", "acmmp_upload_depths", "acmmp_set_state",
     "acmmp_set_scaled_state", "acmmp_set_planar_prior", "acmmp_run_patchmatch", "acmmp_run_patchmatch_ex",
     "acmmp_download", "acmmp_download_aux", "acmmp_device_outputs", "acmmp_synchronize", "acmmp_last_timing",
-    "acmmp_jbu",
+    "acmmp_last_kernel_timing", "acmmp_jbu",
     "acmmp_debug_ncc", "acmmp_debug_geom",
 ]
 
@@ -67,6 +67,7 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_download_aux.argtypes = [vp, vp, vp]
     L.acmmp_device_outputs.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
     L.acmmp_last_timing.argtypes = [vp, vp]
+    L.acmmp_last_kernel_timing.argtypes = [vp, vp, vp]
     L.acmmp_synchronize.argtypes = [vp]
     L.acmmp_jbu.argtypes = [vp, vp, i32, i32, vp, i32, i32, i32, vp]
     L.acmmp_debug_ncc.argtypes = [vp, i32, vp, vp, vp, vp]
@@ -183,6 +184,15 @@ class Context:
         ms = np.zeros(3, np.float32)
         self._check(self.L.acmmp_last_timing(self.h, _p(ms)), "last_timing")
         return {"init_ms": float(ms[0]), "prop_ms": float(ms[1]), "post_ms": float(ms[2])}
+
+    KERNELS = ("k_eval_nb", "k_select", "k_eval_ref", "k_finish")
+
+    def last_kernel_timing(self):
+        """{kernel: (summed ms, launches)} for the half-sweep kernels of the last run."""
+        ms = np.zeros(4, np.float32)
+        n = np.zeros(4, np.int32)
+        self._check(self.L.acmmp_last_kernel_timing(self.h, _p(ms), _p(n)), "last_kernel_timing")
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNELS)}
 
     def jbu(self, ref, coarse, imagescale: int):
         ref = np.ascontiguousarray(ref, np.float32)

@@ -66,6 +66,9 @@ struct acmmp_ctx {
     size_t scratch_bytes = 0;
 
     float timing[3] = {0.f, 0.f, 0.f};
+    std::vector<hipEvent_t> kev;               // 5 per half-sweep (per-kernel timing)
+    float ktiming[4] = {0.f, 0.f, 0.f, 0.f};
+    int klaunch[4] = {0, 0, 0, 0};
     std::string err;
 };
 
@@ -165,6 +168,7 @@ void acmmp_destroy(acmmp_ctx* c) {
         dfree(c->d_sel_cs[k]); dfree(c->d_rng_cs[k]);
     }
     for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->kev) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -441,11 +445,16 @@ acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx* c, uint64_t seed, int n_half_swe
         HIP_TRY(c, hipMemcpyAsync(c->d_cost_cs[k][1], c->d_cost_cs[k][0], sizeof(float) * Pc,
                                   hipMemcpyDeviceToDevice, s));
     }
+    while (c->kev.size() < static_cast<size_t>(5 * n_half_sweeps)) {
+        hipEvent_t e = nullptr;
+        HIP_TRY(c, hipEventCreate(&e));
+        c->kev.push_back(e);
+    }
     HIP_TRY(c, hipEventRecord(c->ev[1], s));
     for (int sw = 0; sw < n_half_sweeps; ++sw) {
         const int colour = sw & 1, iter = sw / 2;
         SweepOut out{c->d_plane_cs[colour][cur[colour] ^ 1], c->d_cost_cs[colour][cur[colour] ^ 1]};
-        HIP_TRY(c, launch_propagate(kp, colour, iter, out, s));
+        HIP_TRY(c, launch_propagate(kp, colour, iter, out, s, &c->kev[5 * sw]));
         cur[colour] ^= 1;
         kp.plane_cs[colour] = c->d_plane_cs[colour][cur[colour]];
         kp.cost_cs[colour] = c->d_cost_cs[colour][cur[colour]];
@@ -462,6 +471,13 @@ acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx* c, uint64_t seed, int n_half_swe
         }
     }
     for (int i = 0; i < 3; ++i) HIP_TRY(c, hipEventElapsedTime(&c->timing[i], c->ev[i], c->ev[i + 1]));
+    for (int k = 0; k < 4; ++k) { c->ktiming[k] = 0.f; c->klaunch[k] = n_half_sweeps; }
+    for (int sw = 0; sw < n_half_sweeps; ++sw)
+        for (int k = 0; k < 4; ++k) {
+            float ms = 0.f;
+            HIP_TRY(c, hipEventElapsedTime(&ms, c->kev[5 * sw + k], c->kev[5 * sw + k + 1]));
+            c->ktiming[k] += ms;
+        }
     return ACMMP_OK;
 }
 
@@ -504,6 +520,12 @@ acmmp_status acmmp_synchronize(acmmp_ctx* c) {
 acmmp_status acmmp_last_timing(const acmmp_ctx* c, float ms[3]) {
     if (!c || !ms) return ACMMP_ERR_INVALID_ARGUMENT;
     for (int i = 0; i < 3; ++i) ms[i] = c->timing[i];
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_last_kernel_timing(const acmmp_ctx* c, float ms[4], int launches[4]) {
+    if (!c || !ms || !launches) return ACMMP_ERR_INVALID_ARGUMENT;
+    for (int k = 0; k < 4; ++k) { ms[k] = c->ktiming[k]; launches[k] = c->klaunch[k]; }
     return ACMMP_OK;
 }
 

@@ -102,7 +102,9 @@ struct SweepOut {
 hipError_t launch_ray_tables(const KParams& kp, float4* dirs, float2* sph_row, float2* sph_col, hipStream_t s);
 hipError_t launch_spatial_table(const KParams& kp, float* spatial, hipStream_t s);
 hipError_t launch_init(const KParams& kp, hipStream_t s);
-hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s);
+// ev: null, or 5 events recorded around the 4 kernels of the half-sweep (per-kernel timing)
+hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s,
+                            hipEvent_t* ev = nullptr);
 hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s);
 hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int sw, int sh, int imagescale,
                       float* out, hipStream_t s);

@@ -1476,16 +1476,24 @@ hipError_t launch_init(const KParams& kp, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s) {
+hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s, hipEvent_t* ev) {
     const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
     const size_t lds_nb = (sizeof(float4) + sizeof(float)) * kNbPix * kp.S + sizeof(float) * 3 * kNbPix;
     const size_t lds_ref = (sizeof(float4) + sizeof(float)) * kRefPix * kp.S + sizeof(float) * 3 * kRefPix;
+    hipError_t e = hipSuccess;
+#define ACMMP_MARK(i) if (ev && (e = hipEventRecord(ev[i], s)) != hipSuccess) return e
+    ACMMP_MARK(0);
     ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC><<<cdiv(npix, kNbPix), 256, lds_nb, s>>>(kp, colour)));
+    ACMMP_MARK(1);
     if (kp.model == kSphere) k_select<kSphere><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter);
     else k_select<kPinhole><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter);
+    ACMMP_MARK(2);
     ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC><<<cdiv(npix, kRefPix), 256, lds_ref, s>>>(kp, colour)));
+    ACMMP_MARK(3);
     if (kp.model == kSphere) k_finish<kSphere><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, out);
     else k_finish<kPinhole><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, out);
+    ACMMP_MARK(4);
+#undef ACMMP_MARK
     return hipGetLastError();
 }
 

@@ -49,6 +49,13 @@ def algorithmic_flop_per_pixel(model: str, V: int, samples: int = 36) -> float:
     return 14 * samples * V * F_HVS[model] + F_SHARED
 
 
+# k_eval_nb -- the dominant kernel: per pixel of a half-sweep it evaluates 9 hypotheses (the 8
+# adaptive-neighbour candidates + the current plane, ACMMP.cu:1151-1170) against every source view:
+# 9 x 36 x (V x F_HVS + 15 shared ray-plane/world-point FLOP) + 36 x 30 bilateral-weight FLOP.
+def eval_nb_flop_per_pixel(model: str, V: int, samples: int = 36) -> float:
+    return 9 * samples * (V * F_HVS[model] + 15.0) + samples * 30.0
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -149,10 +156,14 @@ def main():
     ctx.synchronize()
     t0 = time.perf_counter()
     stage = np.zeros(3)
+    kern = {k: [0.0, 0] for k in capi.Context.KERNELS}
     for k in range(args.steps):
         ctx.run_patchmatch(args.seed + k)
         tm = ctx.last_timing()
         stage += [tm["init_ms"], tm["prop_ms"], tm["post_ms"]]
+        for name, (ms, n) in ctx.last_kernel_timing().items():
+            kern[name][0] += ms
+            kern[name][1] += n
     ctx.synchronize()
     barrier()
     ctx.synchronize()
@@ -168,12 +179,13 @@ def main():
     value = units / t_max / 1e6
     ms_per_step = t_max / args.steps * 1e3
 
-    # roofline of the dominant kernel (k_propagate): mean launch duration from HIP events
-    n_launch = 2 * args.iters * args.steps
-    launch_ms = stage[1] / n_launch
+    # roofline of the dominant kernel (k_eval_nb): mean launch duration from the HIP events the engine
+    # records around every half-sweep kernel on its own stream
+    nb_ms, nb_n = kern["k_eval_nb"]
+    launch_ms = nb_ms / max(nb_n, 1)
     rows = min(args.height, 32 * (((args.height // 2) + 15) // 16))
     pix_per_launch = rows * args.width / 2.0
-    flop_launch = algorithmic_flop_per_pixel(args.model, args.n_src) * pix_per_launch
+    flop_launch = eval_nb_flop_per_pixel(args.model, args.n_src) * pix_per_launch
     achieved = flop_launch / (launch_ms * 1e-3) / 1e12
     traffic = None
     hbm = None
@@ -182,12 +194,12 @@ def main():
             pm = json.load(open(args.pmc))
             if pm.get("config") == {"width": args.width, "height": args.height, "n_src": args.n_src,
                                     "model": args.model}:
-                traffic = pm.get("hbm_bytes_per_launch")
+                traffic = pm.get("kernels", {}).get("k_eval_nb", {}).get("hbm_bytes_per_launch")
                 if traffic:
                     gbs = traffic / (launch_ms * 1e-3) / 1e9
                     hbm = {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                           "frac": round(gbs / PEAK_HBM_GBS, 4)}
-        except (OSError, ValueError):
+                           "frac": round(gbs / PEAK_HBM_GBS, 4), "source": os.path.relpath(args.pmc, REPO)}
+        except (OSError, ValueError, AttributeError):
             pass
     roofline = {
         "bound": "valu",
@@ -196,10 +208,15 @@ def main():
         "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
         "traffic": traffic,
-        "kernel": "k_propagate (CheckerboardPropagation half-sweep)",
+        "kernel": "k_eval_nb (8 neighbour candidates + current plane of a CheckerboardPropagation half-sweep)",
         "launch_ms": round(launch_ms, 4),
+        "launches": nb_n,
         "flop_per_launch": flop_launch,
         "hbm": hbm,
+        "half_sweep_kernels_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items()},
+        "half_sweep_achieved_tflops": round(algorithmic_flop_per_pixel(args.model, args.n_src) / 2.0 *
+                                            rows * args.width / (sum(v[0] for v in kern.values()) /
+                                                                 max(nb_n, 1) * 1e-3) / 1e12, 3),
         "note": "FP32 vector peak (equal to the f32 MFMA dense peak); the path has no GEMM-shaped work",
     }
 

@@ -143,6 +143,11 @@ acmmp_status acmmp_synchronize(acmmp_ctx *ctx);
  * the kernels run on: [init, propagation (all half-sweeps), post]. */
 acmmp_status acmmp_last_timing(const acmmp_ctx *ctx, float ms[3]);
 
+/* Per-kernel device time of the last run's half-sweeps (HIP events around every launch, on the
+ * kernels' stream): summed ms and launch count for [k_eval_nb, k_select, k_eval_ref, k_finish]
+ * (the four kernels one CheckerboardPropagation half-sweep is split into). */
+acmmp_status acmmp_last_kernel_timing(const acmmp_ctx *ctx, float ms[4], int launches[4]);
+
 /* RunJBU / JBU::CudaRun (ACMMP.cpp:1071-1122, ACMMP.cu:1558-1649): joint bilateral
  * upsampling of `coarse` (sw x sh) guided by `ref` (W x H).  imagescale as the
  * reference computes it: max(H / sh, W / sw) (integer division). */

@@ -1,14 +1,32 @@
-"""Summarise rocprofv3 --pmc CSVs: mean counter value per dispatch for each kernel."""
+"""Summarise rocprofv3 --pmc CSVs (scripts/pmc.sh): mean counter value per dispatch for each kernel.
+
+`--json OUT` also writes the traffic summary bench.py reads (profiles/pmc_propagate.json): HBM bytes
+per launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 -- rocprofv3 reports both in KiB, and on gfx950
+FETCH_SIZE counts half the bytes of a wide read (MI355X_MICROARCH.md §HBM; cdna_hip_programming.md
+§counter pitfalls).  Our reads are 8-byte-per-lane bilinear pairs and 16-byte state loads, so the x2
+correction is the guide's prescription, not a calibration of this kernel.
+"""
+import argparse
 import csv
 import glob
 import json
-import sys
+import re
 from collections import defaultdict
+
+SHORT = ("k_eval_nb", "k_select", "k_eval_ref", "k_finish", "k_init", "k_merge", "k_filter", "k_pad_image",
+         "k_ray_tables", "k_spatial", "k_jbu")
+
+
+def short_name(kernel_name: str) -> str:
+    for k in SHORT:
+        if re.search(rf"\b{k}\b", kernel_name):
+            return k
+    return kernel_name
 
 
 def summarize(root):
     per = defaultdict(lambda: defaultdict(list))
-    for path in glob.glob(f"{root}/p*/run_counter_collection.csv"):
+    for path in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
         rows = list(csv.DictReader(open(path)))
         acc = defaultdict(float)
         keyname = {}
@@ -17,7 +35,7 @@ def summarize(root):
             acc[k] += float(r["Counter_Value"])
             keyname[r["Dispatch_Id"]] = r["Kernel_Name"]
         for (d, c), v in acc.items():
-            per[keyname[d]][c].append(v)
+            per[short_name(keyname[d])][c].append(v)
     out = {}
     for kern, cs in per.items():
         out[kern] = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -26,9 +44,30 @@ def summarize(root):
 
 
 if __name__ == "__main__":
-    s = summarize(sys.argv[1])
-    for k, v in s.items():
-        if "propagate" in k or len(sys.argv) > 2:
-            print(k)
-            for c, val in sorted(v.items()):
-                print(f"   {c:28s} {val:,.0f}")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--json")
+    ap.add_argument("--width", type=int, default=2000)
+    ap.add_argument("--height", type=int, default=1500)
+    ap.add_argument("--n-src", type=int, default=4)
+    ap.add_argument("--model", default="sphere")
+    a = ap.parse_args()
+    s = summarize(a.root)
+    for k, v in sorted(s.items()):
+        print(k)
+        for c, val in sorted(v.items()):
+            print(f"   {c:28s} {val:,.1f}")
+    if a.json:
+        kernels = {}
+        for k, v in s.items():
+            if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+                kernels[k] = {"FETCH_SIZE_KiB": v["FETCH_SIZE"], "WRITE_SIZE_KiB": v["WRITE_SIZE"],
+                              "hbm_bytes_per_launch": (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0,
+                              "dispatches": v["_dispatches"]}
+                for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+                          "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "TCC_HIT", "TCC_MISS"):
+                    if c in v:
+                        kernels[k][c] = v[c]
+        json.dump({"config": {"width": a.width, "height": a.height, "n_src": a.n_src, "model": a.model},
+                   "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 bytes per dispatch (gfx950 FETCH_SIZE counts 1/2)",
+                   "kernels": kernels}, open(a.json, "w"), indent=1)
