@@ -193,6 +193,8 @@ acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images,
             return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "bad image " + std::to_string(i));
         if (cams[i].model != ACMMP_PINHOLE && cams[i].model != ACMMP_SPHERE)
             return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "unknown camera model");
+        if (4LL * (cams[i].width + 2) * (cams[i].height + 2) > 0x7fffffffLL)
+            return fail(c, ACMMP_ERR_UNSUPPORTED, "image larger than 2 GiB (32-bit texel offsets)");
         if (cams[i].model != cams[0].model)
             return fail(c, ACMMP_ERR_UNSUPPORTED, "mixed camera models in one problem are not supported");
     }
@@ -250,6 +252,7 @@ acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images,
         d.C[1] = neg_dot3(s.R[1], s.R[4], s.R[7], s.t[0], s.t[1], s.t[2]);
         d.C[2] = neg_dot3(s.R[2], s.R[5], s.R[8], s.t[0], s.t[1], s.t[2]);
         d.img_off = off[i];
+        d.img_bytes = static_cast<int>(4LL * (s.width + 2) * (s.height + 2));
         d.dep_off = 0; d.dep_w = 1; d.dep_h = 1;
     }
     HIP_TRY(c, dalloc(c->d_cams, static_cast<size_t>(n)));

@@ -38,6 +38,8 @@ struct DevCam {
     long long img_off;              // float offset of padded texel (-1,-1)
     long long dep_off;              // float offset of the geom depth map (row-major)
     int dep_w, dep_h;
+    int img_bytes;                  // bytes of the padded image (buffer descriptor range)
+    int pad_;
 };
 
 // Per-pixel state handed from k_select to k_eval_ref / k_finish (80 bytes).

@@ -119,6 +119,19 @@ __device__ __forceinline__ float3 world_point_ray(const DevCam& c, int x, int y,
     }
 }
 
+// sqrtf for the SPHERE projection: LLVM's IEEE f32 sqrt lowering (v_sqrt_f32, then the +-1 ulp
+// fma fix-up) without its small-argument rescale and its +-0/inf class select.  Bit-identical to
+// sqrtf for every x >= 2^-96, +inf and NaN; for smaller x the result is still < 1e-6 and the
+// projection replaces it by the principal point (d < 1e-6 select), and the depth it returns is
+// unused by every caller, so outputs never differ.
+__device__ __forceinline__ float sqrt_proj(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __builtin_bit_cast(float, __builtin_bit_cast(int, s) - 1);
+    const float sup = __builtin_bit_cast(float, __builtin_bit_cast(int, s) + 1);
+    const float r = fmaf(-sdn, s, x) <= 0.0f ? sdn : s;
+    return fmaf(-sup, s, x) > 0.0f ? sup : r;
+}
+
 // ProjectonCamera_cu, ACMMP.cu:602-644 (Cam: DevCam in any address space)
 template <int MODEL, typename Cam>
 __device__ __forceinline__ void project(Cam& c, float3 P, float& ox, float& oy, float& depth) {
@@ -126,7 +139,7 @@ __device__ __forceinline__ void project(Cam& c, float3 P, float& ox, float& oy, 
     const float ty = dot3(c.R[3], c.R[4], c.R[5], P.x, P.y, P.z) + c.t[1];
     const float tz = dot3(c.R[6], c.R[7], c.R[8], P.x, P.y, P.z) + c.t[2];
     if (MODEL == kSphere) {
-        const float d = sqrtf(dot3(tx, ty, tz, tx, ty, tz));
+        const float d = sqrt_proj(dot3(tx, ty, tz, tx, ty, tz));
         depth = d;
         const float neg_lat = det_asin(ty / d);
         const float lon = det_atan2(tx, tz);
@@ -211,6 +224,7 @@ struct Patch {
 };
 
 typedef float float2u __attribute__((ext_vector_type(2), aligned(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // tex2D(img, x+0.5, y+0.5) with fp32 bilinear weights and clamp addressing.  The one-texel
 // replicated border makes (ix, ix+1) valid for ix in [-1, W-1], which equals clamping both,
@@ -223,6 +237,31 @@ __device__ __forceinline__ float bilinear_pair(const float* img, int pitch, int 
     const float* p0 = img + static_cast<long long>(iy + 1) * pitch + (ix + 1);
     const float2u top = *reinterpret_cast<const float2u*>(p0);
     const float2u bot = *reinterpret_cast<const float2u*>(p0 + pitch);
+    const float r0 = fmaf(a, top.y - top.x, top.x);
+    const float r1 = fmaf(a, bot.y - bot.x, bot.x);
+    return fmaf(b, r1 - r0, r0);
+}
+
+// The same fetch through a buffer descriptor of the view's padded image (32-bit texel offsets,
+// 24-bit multiply).  SPHERE callers pass x already wrapped and y clamped to [0, H-1] (never NaN),
+// so y needs no clamp; x keeps clampi(f2i_sat(floor x), -1, W-1): the float clamp below is the
+// same map for every non-NaN value, and NaN -> 0 as f2i_sat does.
+template <bool Y_IN_RANGE>
+__device__ __forceinline__ float bilinear_rsrc(__amdgpu_buffer_rsrc_t rs, int pitch, int W, int H, float x, float y) {
+    const float fx = floorf(x), fy = floorf(y);
+    const float a = x - fx, b = y - fy;
+    int ix = static_cast<int>(fminf(fmaxf(fx, -1.0f), static_cast<float>(W - 1)));
+    ix = fx != fx ? 0 : ix;
+    int iy;
+    if (Y_IN_RANGE) {
+        iy = static_cast<int>(fy);
+    } else {
+        iy = static_cast<int>(fminf(fmaxf(fy, -1.0f), static_cast<float>(H - 1)));
+        iy = fy != fy ? 0 : iy;
+    }
+    const int off = (__mul24(iy + 1, pitch) + ix + 1) * 4;
+    const f32x2 top = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+    const f32x2 bot = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, pitch * 4, 0));
     const float r0 = fmaf(a, top.y - top.x, top.x);
     const float r1 = fmaf(a, bot.y - bot.x, bot.x);
     return fmaf(b, r1 - r0, r0);
@@ -382,7 +421,9 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                     } else {
                         ok = !(sx < 0.0f || sx >= c.Wf || sy < 0.0f || sy >= c.Hf);
                     }
-                    const float sp = bilinear_pair(kp.img + c.img_off, c.img_pitch, c.W, c.H, sx, sy);
+                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                        const_cast<float*>(kp.img + c.img_off), 0, c.img_bytes, 0x00020000);
+                    const float sp = bilinear_rsrc<MODEL == kSphere>(rs, c.img_pitch, c.W, c.H, sx, sy);
                     if (ok) {
                         if (MODEL == kPinhole) {
                             sbw[v] += w;
@@ -870,7 +911,7 @@ __device__ __forceinline__ bool colour_pixel(const KParams& kp, int colour, long
 // stages samples h, h+nh, ...; the first lane of each pixel then forms the SPHERE sums.
 template <int MODEL>
 __device__ __forceinline__ Patch coop_patch(const KParams& kp, bool valid, int px, int py, int lp, int h, int nh,
-                                            float4* lrw, float* lrr, float* lsum) {
+                                            float4* lrw, float* lrr) {
     float4* rw = lrw + lp * kp.S;
     float* rr = lrr + lp * kp.S;
     if (valid) {
@@ -882,13 +923,10 @@ __device__ __forceinline__ Patch coop_patch(const KParams& kp, bool valid, int p
     Patch pt;
     pt.rw = rw; pt.rr = rr; pt.stride = 1;
     pt.center = 0.f;
-    if (MODEL == kSphere && valid && h == 0) {
-        patch_sums<MODEL>(kp, pt);
-        lsum[lp * 3 + 0] = pt.sbw; lsum[lp * 3 + 1] = pt.sref; lsum[lp * 3 + 2] = pt.srr;
-    }
-    __syncthreads();
-    pt.sbw = lsum[lp * 3 + 0]; pt.sref = lsum[lp * 3 + 1]; pt.srr = lsum[lp * 3 + 2];
-    if (MODEL != kSphere) { pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f; }
+    // every lane of the pixel sums its SPHERE weights itself (same order, same bits): no LDS slot
+    // and no second barrier, which keeps k_eval_nb's block at 20160 B of LDS (8 blocks per CU)
+    if (valid) patch_sums<MODEL>(kp, pt);
+    else { pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f; }
     return pt;
 }
 
@@ -902,13 +940,12 @@ __global__ __launch_bounds__(256) void k_eval_nb(const KParams kp, const int col
     extern __shared__ float4 lds4[];
     float4* lrw = lds4;
     float* lrr = reinterpret_cast<float*>(lds4 + kNbPix * kp.S);
-    float* lsum = lrr + kNbPix * kp.S;
     const int t = threadIdx.x;
     const int lp = t / kNbLanes, h = t - lp * kNbLanes;
     const long long q = static_cast<long long>(blockIdx.x) * kNbPix + lp;
     int px = 0, py = 0;
     const bool valid = t < kNbPix * kNbLanes && colour_pixel(kp, colour, q, px, py);
-    const Patch pt = coop_patch<MODEL>(kp, valid, px, py, lp, h, kNbLanes, lrw, lrr, lsum);
+    const Patch pt = coop_patch<MODEL>(kp, valid, px, py, lp, h, kNbLanes, lrw, lrr);
     if (!valid) return;
     const long long Pc = kp.Pc;
     const long long ci = static_cast<long long>(py) * kp.Wh + (px >> 1);
@@ -1208,7 +1245,6 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
     extern __shared__ float4 lds4[];
     float4* lrw = lds4;
     float* lrr = reinterpret_cast<float*>(lds4 + kRefPix * kp.S);
-    float* lsum = lrr + kRefPix * kp.S;
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
     const long long q = static_cast<long long>(blockIdx.x) * kRefPix + lp;
@@ -1224,7 +1260,7 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
         vw = st.vw;
         weight_norm = st.weight_norm;
     }
-    const Patch pt = coop_patch<MODEL>(kp, valid, px, py, lp, h, kRefLanes, lrw, lrr, lsum);
+    const Patch pt = coop_patch<MODEL>(kp, valid, px, py, lp, h, kRefLanes, lrw, lrr);
     if (!valid) return;
     const float4 dc = ray_at<MODEL>(kp, px, py);
     const float4 tp = kp.cand[h * Pc + ci];
@@ -1478,8 +1514,8 @@ hipError_t launch_init(const KParams& kp, hipStream_t s) {
 
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s, hipEvent_t* ev) {
     const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
-    const size_t lds_nb = (sizeof(float4) + sizeof(float)) * kNbPix * kp.S + sizeof(float) * 3 * kNbPix;
-    const size_t lds_ref = (sizeof(float4) + sizeof(float)) * kRefPix * kp.S + sizeof(float) * 3 * kRefPix;
+    const size_t lds_nb = (sizeof(float4) + sizeof(float)) * kNbPix * kp.S;
+    const size_t lds_ref = (sizeof(float4) + sizeof(float)) * kRefPix * kp.S;
     hipError_t e = hipSuccess;
 #define ACMMP_MARK(i) if (ev && (e = hipEventRecord(ev[i], s)) != hipSuccess) return e
     ACMMP_MARK(0);
