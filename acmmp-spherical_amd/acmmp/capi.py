@@ -27,6 +27,8 @@ EXPORTS = [
     "acmmp_download", "acmmp_download_aux", "acmmp_device_outputs", "acmmp_synchronize", "acmmp_last_timing",
     "acmmp_last_kernel_timing", "acmmp_jbu",
     "acmmp_debug_ncc", "acmmp_debug_geom",
+    "acmmp_support_points", "acmmp_delaunay", "acmmp_prior_plane_params", "acmmp_depth_from_plane_param",
+    "acmmp_planar_prior_host",
 ]
 
 
@@ -72,10 +74,17 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_jbu.argtypes = [vp, vp, i32, i32, vp, i32, i32, i32, vp]
     L.acmmp_debug_ncc.argtypes = [vp, i32, vp, vp, vp, vp]
     L.acmmp_debug_geom.argtypes = [vp, i32, vp, vp, vp, vp]
+    L.acmmp_support_points.argtypes = [vp, i32, i32, vp, i32, vp]
+    L.acmmp_delaunay.argtypes = [vp, i32, i32, i32, vp, i32, vp]
+    L.acmmp_prior_plane_params.argtypes = [vp, vp, i32, i32, vp, vp]
+    L.acmmp_depth_from_plane_param.argtypes = [vp, vp, i32, i32]
+    L.acmmp_planar_prior_host.argtypes = [vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]
     for name in EXPORTS:
         fn = getattr(L, name)
-        if name not in ("acmmp_destroy", "acmmp_status_str", "acmmp_last_error", "acmmp_abi_version"):
+        if name not in ("acmmp_destroy", "acmmp_status_str", "acmmp_last_error", "acmmp_abi_version",
+                        "acmmp_depth_from_plane_param"):
             fn.restype = i32
+    L.acmmp_depth_from_plane_param.restype = C.c_float
     _lib = L
     return L
 
@@ -215,3 +224,72 @@ class Context:
 
     def debug_geom(self, px, py, planes):
         return self._debug(self.L.acmmp_debug_geom, px, py, planes)
+
+
+# ---- planar-prior host side (no GPU): ACMMP.cpp:904-1011, main.cpp:113-181 ------------------
+
+def _host_check(rc, what):
+    if rc != 0:
+        raise AcmmpError(f"{what}: {load_library().acmmp_status_str(rc).decode()}")
+
+
+def _cam_ptr(cam):
+    cam = np.frombuffer(np.asarray(cam).tobytes(), dtype=CAMERA_DTYPE).copy()
+    return cam, cam.ctypes.data
+
+
+def support_points(costs) -> np.ndarray:
+    """GetSupportPoints (ACMMP.cpp:904-930) -> (n, 2) int32 (x, y) in the reference's order."""
+    L = load_library()
+    costs = np.ascontiguousarray(costs, np.float32)
+    H, W = costs.shape
+    n = C.c_int(0)
+    L.acmmp_support_points(_p(costs), W, H, None, 0, C.byref(n))
+    xy = np.zeros((max(n.value, 1), 2), np.int32)
+    _host_check(L.acmmp_support_points(_p(costs), W, H, _p(xy), n.value, C.byref(n)), "support_points")
+    return xy[:n.value]
+
+
+def delaunay(xy, W: int, H: int) -> np.ndarray:
+    """DelaunayTriangulation (ACMMP.cpp:932-955) -> (m, 3, 2) int32 triangle vertices."""
+    L = load_library()
+    xy = np.ascontiguousarray(xy, np.int32).reshape(-1, 2)
+    m = C.c_int(0)
+    L.acmmp_delaunay(_p(xy), xy.shape[0], W, H, None, 0, C.byref(m))
+    tri = np.zeros((max(m.value, 1), 3, 2), np.int32)
+    _host_check(L.acmmp_delaunay(_p(xy), xy.shape[0], W, H, _p(tri), m.value, C.byref(m)), "delaunay")
+    return tri[:m.value]
+
+
+def prior_plane_params(cam0, depths, tri) -> np.ndarray:
+    """GetPriorPlaneParams (ACMMP.cpp:957-989) for one triangle ((3, 2) ints)."""
+    L = load_library()
+    depths = np.ascontiguousarray(depths, np.float32)
+    H, W = depths.shape
+    tri = np.ascontiguousarray(tri, np.int32).reshape(6)
+    out = np.zeros(4, np.float32)
+    cam, cp = _cam_ptr(cam0)
+    _host_check(L.acmmp_prior_plane_params(cp, _p(depths), W, H, _p(tri), _p(out)), "prior_plane_params")
+    return out
+
+
+def depth_from_plane_param(cam0, plane, x: int, y: int) -> float:
+    """GetDepthFromPlaneParam (ACMMP.cpp:991-1011)."""
+    plane = np.ascontiguousarray(plane, np.float32)
+    cam, cp = _cam_ptr(cam0)
+    return float(load_library().acmmp_depth_from_plane_param(cp, _p(plane), int(x), int(y)))
+
+
+def planar_prior_host(cam0, depths, costs, depth_min: float, depth_max: float):
+    """main.cpp:113-181 + ACMMP.cpp:851-861 -> (prior_planes (H, W, 4), masks (H, W) uint32, n_triangles)."""
+    L = load_library()
+    depths = np.ascontiguousarray(depths, np.float32)
+    costs = np.ascontiguousarray(costs, np.float32)
+    H, W = depths.shape
+    prior = np.zeros((H, W, 4), np.float32)
+    masks = np.zeros((H, W), np.uint32)
+    n = C.c_int(0)
+    cam, cp = _cam_ptr(cam0)
+    _host_check(L.acmmp_planar_prior_host(cp, _p(depths), _p(costs), W, H, float(depth_min), float(depth_max),
+                                          _p(prior), _p(masks), C.byref(n)), "planar_prior_host")
+    return prior, masks, n.value

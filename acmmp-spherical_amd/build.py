@@ -16,7 +16,8 @@ LIB = os.path.join(HERE, "acmmp", "libacmmp.so")
 ARCH = os.environ.get("ACMMP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["kernels.hip", "capi.cpp"]
+SOURCES = ["kernels.hip", "capi.cpp", "planar_prior.cpp"]
+HIP_CPP = {"capi.cpp"}              # host C++ that includes HIP headers
 HEADERS = ["engine.h", "detmath.h"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}",
           f"-I{INCLUDE}", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
@@ -38,7 +39,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
         srcp = os.path.join(CSRC, src)
         hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "acmmp.h")]
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < _newest([srcp] + hdrs):
-            lang = ["-x", "hip"] if src.endswith(".cpp") else []
+            lang = ["-x", "hip"] if src in HIP_CPP else []
             cmd = [HIPCC, *COMMON, *lang, "-c", srcp, "-o", obj]
             if verbose:
                 print("[acmmp build]", " ".join(cmd), flush=True)

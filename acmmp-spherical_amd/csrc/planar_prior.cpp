@@ -1,0 +1,350 @@
+// planar_prior.cpp -- host side of the planar-prior pass.
+//
+// Restates ACMMP::GetSupportPoints / DelaunayTriangulation / GetPriorPlaneParams /
+// GetDepthFromPlaneParam (ACMMP.cpp:904-1011) and the triangle rasterisation + prior-depth
+// mask of ProcessProblem (main.cpp:113-181) without OpenCV.  Runs on the host (the reference
+// runs it on the host too); compiled with -ffp-contract=off, float/double exactly where the
+// reference's C++ promotes.
+//
+// Delaunay: incremental Bowyer-Watson on the integer support points with exact predicates
+// (64-bit orientation, 128-bit in-circle).  cv::Subdiv2D's triangle order and its choice among
+// co-circular configurations are not reproduced -- that part is "parity unpinned" (SURVEY.md §8c):
+// the device side is pinned by injecting prior planes + masks (acmmp_set_planar_prior).
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "acmmp.h"
+
+namespace {
+
+constexpr double kMPi = 3.14159265358979323846;  // M_PI
+
+struct Pt { long long x, y; };
+
+inline long long orient(const Pt& a, const Pt& b, const Pt& c) {
+    return (b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x);
+}
+
+// > 0 when d lies strictly inside the circumcircle of the counter-clockwise triangle (a, b, c)
+inline int incircle(const Pt& a, const Pt& b, const Pt& c, const Pt& d) {
+    typedef __int128 i128;
+    const i128 adx = a.x - d.x, ady = a.y - d.y, bdx = b.x - d.x, bdy = b.y - d.y, cdx = c.x - d.x, cdy = c.y - d.y;
+    const i128 ad = adx * adx + ady * ady, bd = bdx * bdx + bdy * bdy, cd = cdx * cdx + cdy * cdy;
+    const i128 det = ad * (bdx * cdy - bdy * cdx) - bd * (adx * cdy - ady * cdx) + cd * (adx * bdy - ady * bdx);
+    return det > 0 ? 1 : (det < 0 ? -1 : 0);
+}
+
+struct Tri {
+    int v[3];     // counter-clockwise
+    int nb[3];    // neighbour across the edge opposite v[i]; -1 = none
+    bool alive;
+};
+
+class Delaunay {
+public:
+    explicit Delaunay(std::vector<Pt> pts, long long extent) : p_(std::move(pts)) {
+        const long long M = extent * 4096 + 1024;        // super triangle, far outside the image
+        n_real_ = static_cast<int>(p_.size());
+        p_.push_back({-M, -M});
+        p_.push_back({3 * M, -M});
+        p_.push_back({-M, 3 * M});
+        t_.push_back({{n_real_, n_real_ + 1, n_real_ + 2}, {-1, -1, -1}, true});
+    }
+
+    void run() {
+        for (int i = 0; i < n_real_; ++i) insert(i);
+    }
+
+    // triangles without super vertices, in slot order
+    std::vector<std::array<int, 3>> triangles() const {
+        std::vector<std::array<int, 3>> out;
+        for (const Tri& t : t_) {
+            if (!t.alive) continue;
+            if (t.v[0] >= n_real_ || t.v[1] >= n_real_ || t.v[2] >= n_real_) continue;
+            out.push_back({t.v[0], t.v[1], t.v[2]});
+        }
+        return out;
+    }
+
+private:
+    int locate(const Pt& q) const {
+        int t = last_;
+        if (t < 0 || !t_[t].alive) {
+            for (t = static_cast<int>(t_.size()) - 1; t >= 0 && !t_[t].alive; --t) {}
+        }
+        for (size_t guard = 0; guard < 4 * t_.size() + 16; ++guard) {
+            const Tri& T = t_[t];
+            int next = -1;
+            for (int e = 0; e < 3; ++e) {
+                const Pt& a = p_[T.v[(e + 1) % 3]];
+                const Pt& b = p_[T.v[(e + 2) % 3]];
+                if (orient(a, b, q) < 0) { next = T.nb[e]; break; }
+            }
+            if (next < 0) return t;
+            t = next;
+        }
+        // walk did not converge (cannot happen with exact predicates): fall back to a scan
+        for (int k = 0; k < static_cast<int>(t_.size()); ++k) {
+            if (!t_[k].alive) continue;
+            const Tri& T = t_[k];
+            if (orient(p_[T.v[0]], p_[T.v[1]], q) >= 0 && orient(p_[T.v[1]], p_[T.v[2]], q) >= 0 &&
+                orient(p_[T.v[2]], p_[T.v[0]], q) >= 0)
+                return k;
+        }
+        return 0;
+    }
+
+    int new_tri(int a, int b, int c) {
+        Tri T{{a, b, c}, {-1, -1, -1}, true};
+        if (!free_.empty()) {
+            const int k = free_.back();
+            free_.pop_back();
+            t_[k] = T;
+            return k;
+        }
+        t_.push_back(T);
+        return static_cast<int>(t_.size()) - 1;
+    }
+
+    void insert(int pi) {
+        const Pt& q = p_[pi];
+        const int t0 = locate(q);
+        // cavity: triangles whose circumcircle strictly contains q, connected to t0
+        cavity_.clear();
+        stack_.assign(1, t0);
+        mark_.resize(t_.size(), 0);
+        ++stamp_;
+        if (stamp_ == 0) { std::fill(mark_.begin(), mark_.end(), 0u); stamp_ = 1; }
+        mark_[t0] = stamp_;
+        while (!stack_.empty()) {
+            const int t = stack_.back();
+            stack_.pop_back();
+            cavity_.push_back(t);
+            for (int e = 0; e < 3; ++e) {
+                const int n = t_[t].nb[e];
+                if (n < 0 || mark_[n] == stamp_) continue;
+                const Tri& N = t_[n];
+                if (incircle(p_[N.v[0]], p_[N.v[1]], p_[N.v[2]], q) > 0) {
+                    mark_[n] = stamp_;
+                    stack_.push_back(n);
+                }
+            }
+        }
+        // boundary edges (a, b) of the cavity, counter-clockwise as seen from inside
+        edges_.clear();
+        for (int t : cavity_) {
+            const Tri T = t_[t];
+            for (int e = 0; e < 3; ++e) {
+                const int n = T.nb[e];
+                if (n >= 0 && mark_[n] == stamp_) continue;
+                int slot = -1;
+                if (n >= 0)
+                    for (int k = 0; k < 3; ++k) if (t_[n].nb[k] == t) slot = k;
+                edges_.push_back({T.v[(e + 1) % 3], T.v[(e + 2) % 3], n, slot});
+            }
+        }
+        for (int t : cavity_) { t_[t].alive = false; free_.push_back(t); }
+        // fan from q; new triangle (a, b, q): nb[2] = outer, nb[0] = across (b, q), nb[1] = across (q, a)
+        first_of_.clear();
+        std::vector<int>& made = made_;
+        made.clear();
+        for (const BEdge& E : edges_) {
+            const int k = new_tri(E.a, E.b, pi);
+            if (static_cast<int>(mark_.size()) < static_cast<int>(t_.size())) mark_.resize(t_.size(), 0);
+            t_[k].nb[2] = E.outer;
+            if (E.outer >= 0) t_[E.outer].nb[E.outer_slot] = k;
+            made.push_back(k);
+        }
+        // stitch the fan: triangle with edge starting at vertex a meets the one ending at a
+        for (size_t i = 0; i < made.size(); ++i) first_of_.emplace_back(t_[made[i]].v[0], made[i]);
+        std::sort(first_of_.begin(), first_of_.end());
+        for (int k : made) {
+            const int b = t_[k].v[1];
+            auto it = std::lower_bound(first_of_.begin(), first_of_.end(), std::make_pair(b, -1));
+            const int m = it->second;                    // triangle (b, c, q)
+            t_[k].nb[0] = m;                             // across (b, q)
+            t_[m].nb[1] = k;                             // across (q, b) of m
+        }
+        last_ = made.empty() ? -1 : made.back();
+    }
+
+    struct BEdge { int a, b, outer, outer_slot; };
+    std::vector<Pt> p_;
+    std::vector<Tri> t_;
+    std::vector<int> free_, cavity_, stack_, made_;
+    std::vector<unsigned> mark_;
+    unsigned stamp_ = 0;
+    std::vector<BEdge> edges_;                    // cavity boundary of the current insertion
+    std::vector<std::pair<int, int>> first_of_;
+    int n_real_ = 0;
+    int last_ = 0;
+};
+
+// Get3DPointonRefCam (ACMMP.cpp:287-312), float maths with the reference's promotions
+void point_on_ref_cam(int x, int y, float depth, const acmmp_camera& c, float out[3]) {
+    if (c.model == ACMMP_SPHERE) {
+        const float lon = static_cast<float>((static_cast<float>(x) - c.params[1]) / static_cast<float>(c.width) *
+                                             2.0f * kMPi);
+        const float lat = static_cast<float>(-(static_cast<float>(y) - c.params[2]) /
+                                             static_cast<float>(c.height) * kMPi);
+        out[0] = std::cos(lat) * std::sin(lon) * depth;
+        out[1] = -std::sin(lat) * depth;
+        out[2] = std::cos(lat) * std::cos(lon) * depth;
+    } else {
+        out[0] = depth * (static_cast<float>(x) - c.K[2]) / c.K[0];
+        out[1] = depth * (static_cast<float>(y) - c.K[5]) / c.K[4];
+        out[2] = depth;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+acmmp_status acmmp_support_points(const float* costs, int W, int H, int* xy, int cap, int* n_out) {
+    if (!costs || !n_out || W <= 0 || H <= 0 || cap < 0 || (cap > 0 && !xy)) return ACMMP_ERR_INVALID_ARGUMENT;
+    const int step = 5;
+    int n = 0;
+    for (int col = 0; col < W; col += step) {
+        for (int row = 0; row < H; row += step) {
+            float min_cost = 2.0f;
+            int tx = 0, ty = 0;
+            const int cb = std::min(W, col + step), rb = std::min(H, row + step);
+            for (int c = col; c < cb; ++c)
+                for (int r = row; r < rb; ++r) {
+                    const float v = costs[static_cast<size_t>(r) * W + c];
+                    if (v < 2.0f && min_cost > v) { tx = c; ty = r; min_cost = v; }
+                }
+            if (min_cost < 0.1f) {
+                if (n < cap) { xy[2 * n] = tx; xy[2 * n + 1] = ty; }
+                ++n;
+            }
+        }
+    }
+    *n_out = n;
+    return n <= cap ? ACMMP_OK : ACMMP_ERR_INVALID_ARGUMENT;
+}
+
+acmmp_status acmmp_delaunay(const int* xy, int n, int W, int H, int* tri_xy, int cap, int* n_tri) {
+    if (!n_tri || n < 0 || (n > 0 && !xy) || cap < 0 || (cap > 0 && !tri_xy)) return ACMMP_ERR_INVALID_ARGUMENT;
+    *n_tri = 0;
+    if (n == 0) return ACMMP_OK;                           // ACMMP.cpp:934-936
+    std::vector<Pt> pts(n);
+    for (int i = 0; i < n; ++i) pts[i] = {xy[2 * i], xy[2 * i + 1]};
+    Delaunay d(pts, std::max<long long>(std::max(W, H), 1));
+    d.run();
+    const auto tris = d.triangles();
+    const int m = static_cast<int>(tris.size());
+    for (int k = 0; k < std::min(m, cap); ++k)
+        for (int j = 0; j < 3; ++j) {
+            tri_xy[6 * k + 2 * j] = xy[2 * tris[k][j]];
+            tri_xy[6 * k + 2 * j + 1] = xy[2 * tris[k][j] + 1];
+        }
+    *n_tri = m;
+    return m <= cap ? ACMMP_OK : ACMMP_ERR_INVALID_ARGUMENT;
+}
+
+acmmp_status acmmp_prior_plane_params(const acmmp_camera* cam, const float* depths, int W, int H, const int tri_xy[6],
+                                      float plane[4]) {
+    if (!cam || !depths || !tri_xy || !plane || W <= 0 || H <= 0) return ACMMP_ERR_INVALID_ARGUMENT;
+    float X[3][3];
+    for (int k = 0; k < 3; ++k) {
+        const int x = tri_xy[2 * k], y = tri_xy[2 * k + 1];
+        if (x < 0 || x >= W || y < 0 || y >= H) return ACMMP_ERR_INVALID_ARGUMENT;
+        point_on_ref_cam(x, y, depths[static_cast<size_t>(y) * W + x], *cam, X[k]);
+    }
+    // cv::SVD::solveZ on [X_k 1] (3x4): the null vector, i.e. the plane through the three points
+    // (ACMMP.cpp:960-980).  Closed form: n = (X2-X1) x (X3-X1), w = -n.X1.
+    const float e1[3] = {X[1][0] - X[0][0], X[1][1] - X[0][1], X[1][2] - X[0][2]};
+    const float e2[3] = {X[2][0] - X[0][0], X[2][1] - X[0][1], X[2][2] - X[0][2]};
+    float n4[4] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0], 0.f};
+    n4[3] = -(n4[0] * X[0][0] + n4[1] * X[0][1] + n4[2] * X[0][2]);
+    // ACMMP.cpp:981-988: normalise by the normal's length, sign so that w >= 0
+    float norm2 = static_cast<float>(std::sqrt(std::pow(n4[0], 2) + std::pow(n4[1], 2) + std::pow(n4[2], 2)));
+    if (n4[3] < 0) norm2 *= -1;
+    for (int k = 0; k < 4; ++k) plane[k] = n4[k] / norm2;
+    return ACMMP_OK;
+}
+
+float acmmp_depth_from_plane_param(const acmmp_camera* cam, const float plane[4], int x, int y) {
+    const acmmp_camera& c = *cam;
+    if (c.model == ACMMP_SPHERE) {                          // ACMMP.cpp:993-1006
+        const float lon = static_cast<float>((static_cast<float>(x) - c.params[1]) / static_cast<float>(c.width) *
+                                             2.0f * kMPi);
+        const float lat = static_cast<float>(-(static_cast<float>(y) - c.params[2]) /
+                                             static_cast<float>(c.height) * kMPi);
+        const float dx = std::cos(lat) * std::sin(lon), dy = -std::sin(lat), dz = std::cos(lat) * std::cos(lon);
+        const float denom = plane[0] * dx + plane[1] * dy + plane[2] * dz;
+        return (std::abs(denom) < 1e-6f) ? 1e6f : (-plane[3] / denom);
+    }
+    // ACMMP.cpp:1008-1009 (int x - float K[2] -> float)
+    return -plane[3] * c.K[0] /
+           ((x - c.K[2]) * plane[0] + (c.K[0] / c.K[4]) * (y - c.K[5]) * plane[1] + c.K[0] * plane[2]);
+}
+
+acmmp_status acmmp_planar_prior_host(const acmmp_camera* cam, const float* depths, const float* costs, int W, int H,
+                                     float depth_min, float depth_max, float* prior_planes, uint32_t* masks,
+                                     int* n_triangles) {
+    if (!cam || !depths || !costs || !prior_planes || !masks || W <= 0 || H <= 0) return ACMMP_ERR_INVALID_ARGUMENT;
+    const size_t P = static_cast<size_t>(W) * H;
+    // GetSupportPoints + DelaunayTriangulation (main.cpp:120-121)
+    int n = 0;
+    acmmp_support_points(costs, W, H, nullptr, 0, &n);
+    std::vector<int> xy(2 * static_cast<size_t>(n));
+    acmmp_support_points(costs, W, H, xy.data(), n, &n);
+    int m = 0;
+    acmmp_delaunay(xy.data(), n, W, H, nullptr, 0, &m);
+    std::vector<int> tri(6 * static_cast<size_t>(m));
+    acmmp_delaunay(xy.data(), n, W, H, tri.data(), m, &m);
+    // rasterise every triangle inside the image into the label mask (main.cpp:138-165)
+    std::vector<float> mask_tri(P, 0.0f);
+    std::vector<float> plane_params;
+    uint32_t idx = 0;
+    for (int k = 0; k < m; ++k) {
+        const int* t = &tri[6 * static_cast<size_t>(k)];
+        bool inside = true;
+        for (int j = 0; j < 3; ++j) inside = inside && t[2 * j] >= 0 && t[2 * j] < W && t[2 * j + 1] >= 0 && t[2 * j + 1] < H;
+        if (!inside) continue;
+        const float L01 = static_cast<float>(std::sqrt(std::pow(t[0] - t[2], 2) + std::pow(t[1] - t[3], 2)));
+        const float L02 = static_cast<float>(std::sqrt(std::pow(t[0] - t[4], 2) + std::pow(t[1] - t[5], 2)));
+        const float L12 = static_cast<float>(std::sqrt(std::pow(t[2] - t[4], 2) + std::pow(t[3] - t[5], 2)));
+        const float max_edge_length = std::max(L01, std::max(L02, L12));
+        const float step = static_cast<float>(1.0 / max_edge_length);
+        for (float p = 0; p < 1.0; p += step) {
+            for (float q = 0; q < 1.0 - p; q += step) {
+                const int x = static_cast<int>(static_cast<double>(p * t[0] + q * t[2]) + (1.0 - p - q) * t[4]);
+                const int y = static_cast<int>(static_cast<double>(p * t[1] + q * t[3]) + (1.0 - p - q) * t[5]);
+                mask_tri[static_cast<size_t>(y) * W + x] = static_cast<float>(idx + 1.0);
+            }
+        }
+        float n4[4];
+        acmmp_prior_plane_params(cam, depths, W, H, t, n4);
+        plane_params.insert(plane_params.end(), n4, n4 + 4);
+        ++idx;
+    }
+    // prior depth range check (main.cpp:167-180) and CudaPlanarPriorInitialization (ACMMP.cpp:851-861)
+    for (int i = 0; i < W; ++i) {
+        for (int j = 0; j < H; ++j) {
+            const size_t c = static_cast<size_t>(j) * W + i;
+            if (mask_tri[c] > 0) {
+                const float* pl = &plane_params[4 * (static_cast<size_t>(mask_tri[c]) - 1)];
+                const float d = acmmp_depth_from_plane_param(cam, pl, i, j);
+                if (!(d <= depth_max && d >= depth_min)) mask_tri[c] = 0;
+            }
+        }
+    }
+    for (size_t c = 0; c < P; ++c) {
+        masks[c] = static_cast<uint32_t>(mask_tri[c]);
+        if (mask_tri[c] > 0) std::memcpy(prior_planes + 4 * c, &plane_params[4 * (static_cast<size_t>(mask_tri[c]) - 1)],
+                                         4 * sizeof(float));
+        else std::memset(prior_planes + 4 * c, 0, 4 * sizeof(float));
+    }
+    if (n_triangles) *n_triangles = static_cast<int>(idx);
+    return ACMMP_OK;
+}
+
+}  // extern "C"

@@ -20,6 +20,8 @@ using Camera = acmmp_camera;                 // main.h:189-203
 using PatchMatchParams = acmmp_params;       // ACMMP.h:32-55
 
 struct Float4 { float x, y, z, w; };         // the reference's float4 plane hypothesis
+struct Point { int x, y; };                  // cv::Point
+struct Triangle { Point pt1, pt2, pt3; };    // main.h:66-69
 
 // In-class defaults of PatchMatchParams (ACMMP.h:33-54).
 inline PatchMatchParams DefaultParams() {
@@ -127,6 +129,39 @@ public:
         planes_.resize(P);
         costs_.resize(P);
         ACMMP_SAFE_CALL(acmmp_download(ctx_, &planes_[0].x, costs_.data()));
+    }
+
+    // Planar-prior host helpers (ACMMP.cpp:904-1011) over the C ABI's host functions.
+    void GetSupportPoints(std::vector<Point>& support2DPoints) const {
+        int n = 0;
+        acmmp_support_points(costs_.data(), GetReferenceImageWidth(), GetReferenceImageHeight(), nullptr, 0, &n);
+        std::vector<int> xy(2 * static_cast<size_t>(n));
+        acmmp_support_points(costs_.data(), GetReferenceImageWidth(), GetReferenceImageHeight(), xy.data(), n, &n);
+        support2DPoints.resize(n);
+        for (int i = 0; i < n; ++i) support2DPoints[i] = Point{xy[2 * i], xy[2 * i + 1]};
+    }
+    std::vector<Triangle> DelaunayTriangulation(int width, int height, const std::vector<Point>& points) const {
+        std::vector<int> xy;
+        for (const Point& p : points) { xy.push_back(p.x); xy.push_back(p.y); }
+        int m = 0;
+        const int n = static_cast<int>(points.size());
+        acmmp_delaunay(xy.data(), n, width, height, nullptr, 0, &m);
+        std::vector<int> t(6 * static_cast<size_t>(m));
+        acmmp_delaunay(xy.data(), n, width, height, t.data(), m, &m);
+        std::vector<Triangle> out(m);
+        for (int k = 0; k < m; ++k)
+            out[k] = Triangle{{t[6 * k], t[6 * k + 1]}, {t[6 * k + 2], t[6 * k + 3]}, {t[6 * k + 4], t[6 * k + 5]}};
+        return out;
+    }
+    Float4 GetPriorPlaneParams(const Triangle& tri, const std::vector<float>& depths) const {
+        const int t[6] = {tri.pt1.x, tri.pt1.y, tri.pt2.x, tri.pt2.y, tri.pt3.x, tri.pt3.y};
+        Float4 n4{0, 0, 0, 0};
+        acmmp_prior_plane_params(&cameras_[0], depths.data(), GetReferenceImageWidth(), GetReferenceImageHeight(), t,
+                                 &n4.x);
+        return n4;
+    }
+    float GetDepthFromPlaneParam(const Float4& plane, int x, int y) const {
+        return acmmp_depth_from_plane_param(&cameras_[0], &plane.x, x, y);
     }
 
     int GetReferenceImageWidth() const { return cameras_[0].width; }

@@ -31,5 +31,23 @@ int main() {
     double mean_depth = 0.0;
     for (int i = 0; i < width * height; ++i) mean_depth += acmmp.GetPlaneHypothesis(i).w;  // main.cpp:103-111
     std::printf("mean depth %.4f over %dx%d\n", mean_depth / (width * height), width, height);
+
+    // planar pass (main.cpp:113-187): support points, Delaunay, per-triangle planes, second run
+    std::vector<float> depths(width * height);
+    for (int i = 0; i < width * height; ++i) depths[i] = acmmp.GetPlaneHypothesis(i).w;
+    acmmp.SetPlanarPriorParams();
+    std::vector<Point> support;
+    acmmp.GetSupportPoints(support);
+    const std::vector<Triangle> triangles = acmmp.DelaunayTriangulation(width, height, support);
+    std::vector<float> mask_tri(width * height, 0.0f);
+    std::vector<Float4> planes;
+    for (const Triangle& t : triangles) {
+        planes.push_back(acmmp.GetPriorPlaneParams(t, depths));
+        const int cx = (t.pt1.x + t.pt2.x + t.pt3.x) / 3, cy = (t.pt1.y + t.pt2.y + t.pt3.y) / 3;
+        mask_tri[cy * width + cx] = static_cast<float>(planes.size());   // centroid label only (example)
+    }
+    acmmp.CudaPlanarPriorInitialization(planes, mask_tri);
+    acmmp.RunPatchMatch();
+    std::printf("planar pass: %zu support points, %zu triangles\n", support.size(), triangles.size());
     return 0;
 }

@@ -148,6 +148,35 @@ acmmp_status acmmp_last_timing(const acmmp_ctx *ctx, float ms[3]);
  * (the four kernels one CheckerboardPropagation half-sweep is split into). */
 acmmp_status acmmp_last_kernel_timing(const acmmp_ctx *ctx, float ms[4], int launches[4]);
 
+/* ---- planar-prior host side (no GPU; ACMMP.cpp:904-1011, main.cpp:113-181) ---------------
+ * Host restatements of the reference's planar-prior helpers, so a caller can run ProcessProblem's
+ * planar pass without OpenCV.  Delaunay ties / triangle order differ from cv::Subdiv2D
+ * (parity unpinned).  Output arrays are caller-allocated; when `cap` is too small
+ * the call returns ACMMP_ERR_INVALID_ARGUMENT with the required count in *n_out / *n_tri. */
+
+/* ACMMP::GetSupportPoints (ACMMP.cpp:904-930): per 5x5 tile the min-cost pixel if cost < 0.1;
+ * xy = (x, y) pairs in the reference's order (tile columns outer, tile rows inner). */
+acmmp_status acmmp_support_points(const float *costs, int W, int H, int *xy, int cap, int *n_out);
+
+/* ACMMP::DelaunayTriangulation (ACMMP.cpp:932-955): triangles as 6 ints (x1 y1 x2 y2 x3 y3). */
+acmmp_status acmmp_delaunay(const int *xy, int n, int W, int H, int *tri_xy, int cap, int *n_tri);
+
+/* ACMMP::GetPriorPlaneParams (ACMMP.cpp:957-989): plane (n, w), |n| = 1, w >= 0, through the
+ * triangle's three reference-camera points at `depths` (W x H). */
+acmmp_status acmmp_prior_plane_params(const acmmp_camera *cam0, const float *depths, int W, int H,
+                                      const int tri_xy[6], float plane[4]);
+
+/* ACMMP::GetDepthFromPlaneParam (ACMMP.cpp:991-1011). */
+float acmmp_depth_from_plane_param(const acmmp_camera *cam0, const float plane[4], int x, int y);
+
+/* The planar block of ProcessProblem (main.cpp:113-181) + CudaPlanarPriorInitialization's
+ * expansion (ACMMP.cpp:851-861): support points, Delaunay, rasterised triangle labels, per-triangle
+ * planes, prior-depth range mask -> per-pixel prior planes (float4[P]) and labels (u32[P]) ready for
+ * acmmp_set_planar_prior.  depths/costs: the first RunPatchMatch's output. */
+acmmp_status acmmp_planar_prior_host(const acmmp_camera *cam0, const float *depths, const float *costs, int W,
+                                     int H, float depth_min, float depth_max, float *prior_planes,
+                                     uint32_t *masks, int *n_triangles);
+
 /* RunJBU / JBU::CudaRun (ACMMP.cpp:1071-1122, ACMMP.cu:1558-1649): joint bilateral
  * upsampling of `coarse` (sw x sh) guided by `ref` (W x H).  imagescale as the
  * reference computes it: max(H / sh, W / sw) (integer division). */
