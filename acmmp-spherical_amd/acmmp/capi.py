@@ -29,6 +29,9 @@ EXPORTS = [
     "acmmp_debug_ncc", "acmmp_debug_geom",
     "acmmp_support_points", "acmmp_delaunay", "acmmp_prior_plane_params", "acmmp_depth_from_plane_param",
     "acmmp_planar_prior_host",
+    "acmmp_upload_depths_device", "acmmp_export_depth", "acmmp_device_alloc", "acmmp_device_free", "acmmp_memcpy",
+    "acmmp_comm_unique_id", "acmmp_comm_create", "acmmp_comm_destroy", "acmmp_comm_broadcast",
+    "acmmp_comm_allreduce_max",
 ]
 
 
@@ -78,11 +81,21 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_delaunay.argtypes = [vp, i32, i32, i32, vp, i32, vp]
     L.acmmp_prior_plane_params.argtypes = [vp, vp, i32, i32, vp, vp]
     L.acmmp_depth_from_plane_param.argtypes = [vp, vp, i32, i32]
+    L.acmmp_upload_depths_device.argtypes = [vp, i32, vp, vp, vp]
+    L.acmmp_export_depth.argtypes = [vp, vp]
+    L.acmmp_device_alloc.argtypes = [i32, C.c_size_t, C.POINTER(vp)]
+    L.acmmp_device_free.argtypes = [i32, vp]
+    L.acmmp_memcpy.argtypes = [i32, vp, vp, C.c_size_t, i32]
+    L.acmmp_comm_unique_id.argtypes = [vp]
+    L.acmmp_comm_create.argtypes = [i32, vp, i32, i32, C.POINTER(vp)]
+    L.acmmp_comm_destroy.argtypes = [vp]
+    L.acmmp_comm_broadcast.argtypes = [vp, i32, vp, vp, vp]
+    L.acmmp_comm_allreduce_max.argtypes = [vp, vp, i32]
     L.acmmp_planar_prior_host.argtypes = [vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]
     for name in EXPORTS:
         fn = getattr(L, name)
         if name not in ("acmmp_destroy", "acmmp_status_str", "acmmp_last_error", "acmmp_abi_version",
-                        "acmmp_depth_from_plane_param"):
+                        "acmmp_depth_from_plane_param", "acmmp_comm_destroy"):
             fn.restype = i32
     L.acmmp_depth_from_plane_param.restype = C.c_float
     _lib = L
@@ -149,6 +162,19 @@ class Context:
         w = np.array([d.shape[1] for d in ds], np.int32)
         h = np.array([d.shape[0] for d in ds], np.int32)
         self._check(self.L.acmmp_upload_depths(self.h, n, C.cast(ptrs, C.c_void_p), _p(w), _p(h)), "upload_depths")
+
+    def upload_depths_device(self, bufs):
+        """bufs: DeviceBuffer depth maps (index 0 = reference) on this context's GPU."""
+        n = len(bufs)
+        ptrs = (C.c_void_p * n)(*[b.ptr for b in bufs])
+        w = np.array([b.shape[1] for b in bufs], np.int32)
+        h = np.array([b.shape[0] for b in bufs], np.int32)
+        self._check(self.L.acmmp_upload_depths_device(self.h, n, C.cast(ptrs, C.c_void_p), _p(w), _p(h)),
+                    "upload_depths_device")
+
+    def export_depth(self, buf):
+        """Copy the last run's depth map into DeviceBuffer `buf` (H x W floats)."""
+        self._check(self.L.acmmp_export_depth(self.h, C.c_void_p(buf.ptr)), "export_depth")
 
     def set_state(self, planes=None, costs=None):
         pl = None if planes is None else np.ascontiguousarray(planes, np.float32)
@@ -293,3 +319,77 @@ def planar_prior_host(cam0, depths, costs, depth_min: float, depth_max: float):
     _host_check(L.acmmp_planar_prior_host(cp, _p(depths), _p(costs), W, H, float(depth_min), float(depth_max),
                                           _p(prior), _p(masks), C.byref(n)), "planar_prior_host")
     return prior, masks, n.value
+
+
+# ---- device buffers + RCCL communicator (multi-GPU pipeline) ---------------------
+
+class DeviceBuffer:
+    """A float32 (H, W) buffer in HBM of one GPU (pipeline depth store)."""
+
+    def __init__(self, device: int, shape):
+        self.L = load_library()
+        self.device, self.shape = device, tuple(int(v) for v in shape)
+        self.nbytes = 4 * int(np.prod(self.shape))
+        p = C.c_void_p()
+        _host_check(self.L.acmmp_device_alloc(device, self.nbytes, C.byref(p)), "device_alloc")
+        self.ptr = p.value
+
+    def upload(self, arr):
+        a = np.ascontiguousarray(arr, np.float32)
+        assert a.shape == self.shape
+        _host_check(self.L.acmmp_memcpy(self.device, C.c_void_p(self.ptr), _p(a), self.nbytes, 0), "memcpy H2D")
+
+    def download(self):
+        a = np.empty(self.shape, np.float32)
+        _host_check(self.L.acmmp_memcpy(self.device, _p(a), C.c_void_p(self.ptr), self.nbytes, 1), "memcpy D2H")
+        return a
+
+    def free(self):
+        if self.ptr:
+            self.L.acmmp_device_free(self.device, C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Comm:
+    """RCCL communicator of this process's GPU (one rank per process)."""
+
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * Comm.ID_BYTES)()
+        _host_check(load_library().acmmp_comm_unique_id(C.cast(buf, C.c_void_p)), "comm_unique_id")
+        return bytes(buf)
+
+    def __init__(self, device: int, uid: bytes, nranks: int, rank: int):
+        self.L = load_library()
+        assert len(uid) == self.ID_BYTES
+        buf = (C.c_uint8 * self.ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        _host_check(self.L.acmmp_comm_create(device, C.cast(buf, C.c_void_p), nranks, rank, C.byref(h)),
+                    "comm_create")
+        self.h, self.nranks, self.rank = h, nranks, rank
+
+    def broadcast(self, bufs, roots):
+        """In-place grouped broadcast of DeviceBuffers, bufs[i] from rank roots[i]."""
+        n = len(bufs)
+        ptrs = (C.c_void_p * n)(*[b.ptr for b in bufs])
+        nb = np.array([b.nbytes for b in bufs], np.uint64)
+        rt = np.array(roots, np.int32)
+        _host_check(self.L.acmmp_comm_broadcast(self.h, n, C.cast(ptrs, C.c_void_p), _p(nb), _p(rt)), "broadcast")
+
+    def allreduce_max(self, vals):
+        v = np.ascontiguousarray(vals, np.float64).copy()
+        _host_check(self.L.acmmp_comm_allreduce_max(self.h, _p(v), v.size), "allreduce_max")
+        return v
+
+    def close(self):
+        if self.h:
+            self.L.acmmp_comm_destroy(self.h)
+            self.h = None

@@ -1,0 +1,434 @@
+"""Multi-view, multi-scale pipeline driver.
+
+Restates the reference's scheduler (main.cpp:392-482), ProcessProblem (main.cpp:73-210),
+JointBilateralUpsampling (main.cpp:212-238) and the host half of InuputInitialization /
+CudaSpaceInitialization (ACMMP.cpp:567-845) over the C ABI -- with the dmb round trip between
+passes replaced by an in-memory depth store:
+
+* each process drives one GPU (one `capi.Context`, reused for every ProcessProblem);
+* reference views are sharded over the ranks (`owner(i) = i % world`, no data-path collective
+  inside a pass);
+* between passes, the depth maps a geometric-consistency pass reads are broadcast from their
+  owners HBM-to-HBM (RCCL over xGMI, `RcclExchange`) and uploaded device-to-device;
+* dmb files are still written (optional) so a reference user finds the usual outputs.
+
+Pass ordering.  The reference runs each pass's views one after another, and a geom pass with
+multi_geometry reads the depths_geom.dmb its predecessors in the SAME pass have just rewritten
+(main.cpp:443-445 + ACMMP.cpp:653-664).  `order="reference"` reproduces that (single rank);
+`order="snapshot"` lets every view of a pass read the previous pass's maps (Jacobi order), which
+is what a sharded multi-GPU run does.  Everything else is identical.
+
+Seeds.  The reference seeds from clock64(); here every RunPatchMatch gets
+seed + 7919 * pass + 31 * ref_image_id + run.
+"""
+from __future__ import annotations
+
+import copy
+import math
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import capi, io, types
+
+
+# ---------------------------------------------------------------- inputs
+
+@dataclass
+class Dataset:
+    """What the reference reads from a dense folder: grey images (float32, full size), cameras
+    (ReadCamera, width/height = image size) and the problems of pair.txt (indexed by image id,
+    as the reference indexes problems[src_id], ACMMP.cpp:611)."""
+    images: dict
+    cameras: dict
+    problems: list
+    folder: str | None = None
+
+
+def read_gray(path: str) -> np.ndarray:
+    """cv::imread(IMREAD_GRAYSCALE) + convertTo(CV_32F) (ACMMP.cpp:578-580).  PIL decodes the JPEG
+    luma plane directly (draft 'L'); decoder differences vs OpenCV's libjpeg build are not pinned."""
+    from PIL import Image
+    with Image.open(path) as im:
+        if im.format == "JPEG":
+            im.draft("L", im.size)
+        return np.asarray(im.convert("L"), dtype=np.float32).copy()
+
+
+def load_dataset(dense_folder: str) -> Dataset:
+    problems = io.read_pair_list(dense_folder)
+    images, cameras = {}, {}
+    for p in problems:
+        i = p.ref_image_id
+        images[i] = read_gray(os.path.join(dense_folder, "images", f"{i:08d}.jpg"))
+        cam = io.read_camera(os.path.join(dense_folder, "cams", f"{i:08d}_cam.txt"))
+        cam["height"], cam["width"] = images[i].shape
+        cameras[i] = cam
+    return Dataset(images, cameras, problems, dense_folder)
+
+
+def resize_linear(img: np.ndarray, new_cols: int, new_rows: int) -> np.ndarray:
+    """cv::resize(INTER_LINEAR) of a float32 image (resizeGeneric_: HResizeLinear then VResizeLinear
+    with float coefficients; source coordinate (d + 0.5) * scale - 0.5, clamped at the borders).
+    OpenCV's SIMD kernels may fuse the multiply-adds: parity with cv::resize is unpinned."""
+    src = np.ascontiguousarray(img, np.float32)
+    rows, cols = src.shape
+
+    def taps(dsize, ssize):
+        scale = ssize / dsize
+        d = np.arange(dsize, dtype=np.float64)
+        f = ((d + 0.5) * scale - 0.5).astype(np.float32)
+        s = np.floor(f).astype(np.int64)
+        f = (f - s.astype(np.float32)).astype(np.float32)
+        lo = s < 0
+        f[lo], s[lo] = 0.0, 0
+        hi = s >= ssize - 1
+        f[hi], s[hi] = 0.0, ssize - 1
+        s1 = np.minimum(s + 1, ssize - 1)
+        return s, s1, (np.float32(1.0) - f).astype(np.float32), f
+
+    xs0, xs1, ax0, ax1 = taps(new_cols, cols)
+    ys0, ys1, by0, by1 = taps(new_rows, rows)
+    h = (src[:, xs0] * ax0 + src[:, xs1] * ax1).astype(np.float32)
+    return (h[ys0] * by0[:, None] + h[ys1] * by1[:, None]).astype(np.float32)
+
+
+def scale_view(image: np.ndarray, cam: np.ndarray, max_image_size: int):
+    """InuputInitialization's per-view rescale (ACMMP.cpp:607-643): only when the image exceeds
+    max_image_size; SPHERE scales (cx, cy), PINHOLE scales K."""
+    cam = np.array(cam, copy=True)
+    rows, cols = image.shape
+    if cols <= max_image_size and rows <= max_image_size:
+        return image, cam
+    factor = min(np.float32(max_image_size) / np.float32(cols), np.float32(max_image_size) / np.float32(rows))
+    new_cols = int(np.round(np.float32(cols) * factor))
+    new_rows = int(np.round(np.float32(rows) * factor))
+    sx = np.float32(new_cols) / np.float32(cols)
+    sy = np.float32(new_rows) / np.float32(rows)
+    out = resize_linear(image, new_cols, new_rows)
+    if int(cam["model"]) == types.SPHERE:
+        cam["params"][1] = np.float32(cam["params"][1] * sx)
+        cam["params"][2] = np.float32(cam["params"][2] * sy)
+    else:
+        K = cam["K"]
+        K[0] = np.float32(K[0] * sx); K[2] = np.float32(K[2] * sx)
+        K[4] = np.float32(K[4] * sy); K[5] = np.float32(K[5] * sy)
+        cam["K"] = K
+    cam["height"], cam["width"] = out.shape
+    return out, cam
+
+
+# ---------------------------------------------------------------- depth exchange between ranks
+
+class LocalExchange:
+    """Single rank: every view is local, nothing to move."""
+    world, rank = 1, 0
+
+    def share(self, key, views, owners, store):
+        pass
+
+    def close(self):
+        pass
+
+
+class RcclExchange:
+    """Depth maps live in HBM (DeviceBuffer per (key, view)); a pass's outputs are broadcast from
+    their owners with one grouped RCCL call."""
+
+    def __init__(self, comm: capi.Comm, device: int):
+        self.comm, self.device = comm, device
+        self.world, self.rank = comm.nranks, comm.rank
+
+    def share(self, key, views, owners, store):
+        bufs = [store.device_map(key, v) for v in views]
+        self.comm.broadcast(bufs, [owners[v] for v in views])
+        for v in views:
+            if owners[v] != self.rank:
+                store.host.pop((key, v), None)      # re-read from HBM on demand
+
+    def close(self):
+        self.comm.close()
+
+
+class ViewStore:
+    """What the reference keeps in ACMMP/2333_<id>/{depths,depths_geom,normals,costs}.dmb."""
+
+    def __init__(self, device: int | None):
+        self.device = device
+        self.host = {}                               # (key, view) -> np.ndarray
+        self.dev = {}                                # (key, view) -> capi.DeviceBuffer
+        self.shapes = {}                             # (key, view) -> (H, W)
+
+    def put(self, key, view, arr, ctx=None):
+        arr = np.ascontiguousarray(arr, np.float32)
+        self.host[(key, view)] = arr
+        self.shapes[(key, view)] = arr.shape
+        if self.device is not None and key in ("depths", "depths_geom"):
+            buf = self.device_map(key, view, arr.shape)
+            if ctx is not None and hasattr(ctx, "export_depth"):
+                ctx.export_depth(buf)                # HBM -> HBM, no host round trip
+            else:
+                buf.upload(arr)
+
+    def device_map(self, key, view, shape=None):
+        b = self.dev.get((key, view))
+        shape = shape or self.shapes[(key, view)]
+        if b is None or b.shape != tuple(shape):
+            if b is not None:
+                b.free()
+            b = capi.DeviceBuffer(self.device, shape)
+            self.dev[(key, view)] = b
+            self.shapes[(key, view)] = tuple(shape)
+        return b
+
+    def get(self, key, view):
+        a = self.host.get((key, view))
+        if a is None and (key, view) in self.dev:
+            a = self.dev[(key, view)].download()
+            self.host[(key, view)] = a
+        return a
+
+    def has(self, key, view):
+        return (key, view) in self.host or (key, view) in self.dev
+
+
+# ---------------------------------------------------------------- the driver
+
+@dataclass
+class PassLog:
+    name: str
+    views: list = field(default_factory=list)
+
+
+class Pipeline:
+    """main.cpp's main loop over a Dataset, sharded over `exchange.world` ranks."""
+
+    def __init__(self, ds: Dataset, engine=None, exchange=None, device: int = 0, seed: int = 1234,
+                 order: str = "reference", geom_iterations: int = 2, out_folder: str | None = None,
+                 use_device_store: bool | None = None, size_bound: int = 1000, max_image_size: int = 3200,
+                 log=None):
+        self.ds = ds
+        self.exchange = exchange or LocalExchange()
+        self.world, self.rank = self.exchange.world, self.exchange.rank
+        if self.world > 1 and order == "reference":
+            raise ValueError("order='reference' is sequential over views; sharded runs use order='snapshot'")
+        if order not in ("reference", "snapshot"):
+            raise ValueError(order)
+        self.order = order
+        self.engine = engine if engine is not None else capi.Context(device)
+        gpu = isinstance(self.engine, capi.Context)
+        self.store = ViewStore(device if (gpu if use_device_store is None else use_device_store) else None)
+        self.seed = seed
+        self.geom_iterations = geom_iterations
+        self.size_bound, self.max_image_size = size_bound, max_image_size
+        self.out_folder = out_folder
+        self.log = log or (lambda *a: None)
+        self.problems = copy.deepcopy(ds.problems)
+        self.pass_index = 0
+        self.passes = []
+        self._pending = []
+
+    # -- sharding
+    def owner(self, i: int) -> int:
+        return i % self.world
+
+    def my_problems(self):
+        return [i for i in range(len(self.problems)) if self.owner(i) == self.rank]
+
+    # -- the schedule (main.cpp:392-482, fusion excluded)
+    def run(self):
+        sizes = {p.ref_image_id: self.ds.images[p.ref_image_id].shape for p in self.problems}
+        max_num_downscale = io.compute_multiscale_settings(self.problems, sizes, self.max_image_size,
+                                                           self.size_bound)
+        flag = 0
+        while max_num_downscale >= 0:
+            for p in self.problems:
+                if p.num_downscale >= 0:
+                    p.cur_image_size = int(p.max_image_size / (2 ** p.num_downscale))
+                    p.num_downscale -= 1
+            if flag == 0:
+                flag = 1
+                self._pass(geom=False, planar=True, hier=False, multi=False)
+            else:
+                for i in self.my_problems():
+                    self.joint_bilateral_upsampling(i, self.problems[i].cur_image_size)
+                self._pass(geom=False, planar=True, hier=True, multi=False)
+            for g in range(self.geom_iterations):
+                self._pass(geom=True, planar=False, hier=False, multi=g > 0)
+            max_num_downscale -= 1
+        return self
+
+    def _pass(self, geom, planar, hier, multi):
+        name = ("geom" + ("_multi" if multi else "")) if geom else ("hier_planar" if hier else "planar")
+        self.log(f"[rank {self.rank}] pass {self.pass_index}: {name}")
+        log = PassLog(name)
+        for i in self.my_problems():
+            self.process_problem(i, geom, planar, hier, multi)
+            log.views.append(self.problems[i].ref_image_id)
+        self._commit_pending()
+        key = "depths_geom" if geom else "depths"
+        if self.world > 1:
+            views = [p.ref_image_id for p in self.problems]
+            owners = {self.problems[i].ref_image_id: self.owner(i) for i in range(len(self.problems))}
+            for v in views:
+                if owners[v] != self.rank:
+                    self.store.shapes[(key, v)] = self._pass_shape(v)
+            self.exchange.share(key, views, owners, self.store)
+        self.passes.append(log)
+        self.pass_index += 1
+
+    def _pass_shape(self, view_id):
+        img, _ = scale_view(self.ds.images[view_id], self.ds.cameras[view_id], self.problems[view_id].cur_image_size)
+        return img.shape
+
+    def _commit_pending(self):
+        for key, view, arr, ctx in self._pending:
+            self.store.put(key, view, arr)
+        self._pending = []
+
+    def _save(self, key, view, arr, export_ctx=None):
+        if self.order == "snapshot" and key in ("depths", "depths_geom"):
+            self._pending.append((key, view, arr, None))
+        else:
+            self.store.put(key, view, arr, export_ctx)
+
+    # -- InuputInitialization (ACMMP.cpp:567-679)
+    def _inputs(self, idx):
+        prob = self.problems[idx]
+        ids = [prob.ref_image_id] + list(prob.src_image_ids)
+        images, cams = [], []
+        for k, vid in enumerate(ids):
+            size = prob.cur_image_size if k == 0 else self.problems[vid].cur_image_size
+            img, cam = scale_view(self.ds.images[vid], self.ds.cameras[vid], size)
+            images.append(img)
+            cams.append(cam)
+        return ids, images, np.array(cams, dtype=types.CAMERA_DTYPE)
+
+    # -- ProcessProblem (main.cpp:73-210)
+    def process_problem(self, idx, geom, planar, hier, multi):
+        prob = self.problems[idx]
+        ref = prob.ref_image_id
+        ids, images, cams = self._inputs(idx)
+        c0 = cams[0]
+        p = types.default_params(num_images=len(images), depth_min=float(c0["depth_min"]) * 0.6,
+                                 depth_max=float(c0["depth_max"]) * 1.2)
+        p["depth_min"] = np.float32(c0["depth_min"] * np.float32(0.6))
+        p["depth_max"] = np.float32(c0["depth_max"] * np.float32(1.2))
+        if geom:                                                     # SetGeomConsistencyParams
+            p["geom_consistency"] = 1
+            p["max_iterations"] = 2
+            p["multi_geometry"] = int(multi)
+        if hier:
+            p["hierarchy"] = 1
+        e = self.engine
+        H, W = images[0].shape
+        if geom:
+            key = "depths_geom" if multi else "depths"
+            e.set_params(p)
+            e.upload_views(images, cams)
+            if self.store.device is not None and hasattr(e, "upload_depths_device"):
+                e.upload_depths_device([self.store.device_map(key, v) for v in ids])
+            else:
+                e.upload_depths([self.store.get(key, v) for v in ids])
+            depth = self.store.get(key, ref)
+            normals = self.store.get("normals", ref)
+            costs = self.store.get("costs", ref)
+            planes = np.concatenate([normals, depth[..., None]], axis=-1)
+            e.set_state(planes, costs)
+        elif hier:
+            depth = self.store.get("depths", ref)                    # JBU output, fine size
+            normals = self.store.get("normals", ref)                 # previous scale
+            costs = self.store.get("costs", ref)
+            sh, sw = normals.shape[:2]
+            if sw != W or sh != H:
+                p["upsample"] = 1
+                p["scaled_cols"] = np.float32(sw)
+                p["scaled_rows"] = np.float32(sh)
+                scaled = np.concatenate([normals, costs[..., None]], axis=-1)
+            else:
+                p["upsample"] = 0
+                scaled = np.concatenate([normals, depth[..., None]], axis=-1)
+            e.set_params(p)
+            e.upload_views(images, cams)
+            e.set_scaled_state(scaled)
+            state = np.zeros((H, W, 4), np.float32)
+            state[..., 3] = depth[:H, :W] if depth.shape == (H, W) else 0.0
+            e.set_state(state, None)
+        else:
+            e.set_params(p)
+            e.upload_views(images, cams)
+        run_seed = self.seed + 7919 * self.pass_index + 31 * ref
+        e.run_patchmatch(run_seed)
+        planes, costs = e.download()
+        if planar:                                                   # main.cpp:113-187
+            p["planar_prior"] = 1
+            prior, masks, _ = capi.planar_prior_host(c0, planes[..., 3], costs, float(p["depth_min"]),
+                                                     float(p["depth_max"]))
+            e.set_params(p)
+            e.set_planar_prior(prior, masks)
+            e.run_patchmatch(run_seed + 1)
+            planes, costs = e.download()
+        key = "depths_geom" if geom else "depths"
+        self._save(key, ref, planes[..., 3].copy(), e if isinstance(e, capi.Context) else None)
+        self.store.put("normals", ref, planes[..., :3].copy())
+        self.store.put("costs", ref, costs)
+        if self.out_folder:
+            d = os.path.join(self.out_folder, "ACMMP", f"2333_{ref:08d}")
+            os.makedirs(d, exist_ok=True)
+            io.write_dmb(os.path.join(d, key + ".dmb"), planes[..., 3])
+            io.write_dmb(os.path.join(d, "normals.dmb"), planes[..., :3])
+            io.write_dmb(os.path.join(d, "costs.dmb"), costs)
+        return planes, costs
+
+    # -- JointBilateralUpsampling (main.cpp:212-238) + RunJBU (ACMMP.cpp:1071-1122)
+    def joint_bilateral_upsampling(self, idx, acmmp_size):
+        ref = self.problems[idx].ref_image_id
+        coarse = self.store.get("depths_geom", ref)
+        img = self.ds.images[ref]
+        rows, cols = img.shape
+        factor = min(np.float32(acmmp_size) / np.float32(cols), np.float32(acmmp_size) / np.float32(rows))
+        new_cols = int(np.round(np.float32(cols) * factor))
+        new_rows = int(np.round(np.float32(rows) * factor))
+        scaled = resize_linear(img, new_cols, new_rows)
+        imagescale = max(scaled.shape[0] // coarse.shape[0], scaled.shape[1] // coarse.shape[1])
+        if imagescale == 1:                                          # ACMMP.cpp:1076-1079
+            return None
+        out = self.engine.jbu(scaled, coarse, imagescale)
+        self.store.put("depths", ref, out)
+        if self.out_folder:
+            d = os.path.join(self.out_folder, "ACMMP", f"2333_{ref:08d}")
+            os.makedirs(d, exist_ok=True)
+            io.write_dmb(os.path.join(d, "depths.dmb"), out)
+        return out
+
+
+def launcher_store():
+    """The torchrun launcher's TCP key-value store (host bytes only).  Under torchrun the agent hosts
+    it at MASTER_ADDR:MASTER_PORT (TORCHELASTIC_USE_AGENT_STORE); otherwise rank 0 hosts it there."""
+    from torch.distributed import TCPStore
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+    return TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]), world,
+                    is_master=(rank == 0 and not agent), wait_for_workers=False)
+
+
+def comm_from_env(device: int, tag: str = "acmmp"):
+    """RCCL communicator of a torchrun-launched process: rank 0 makes the unique id and publishes it
+    in the launcher's store; the data path is RCCL."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    store = launcher_store()
+    key = f"{tag}_uid_{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}"
+    if rank == 0:
+        store.set(key, capi.Comm.unique_id())
+    uid = store.get(key)
+    return capi.Comm(device, uid, world, rank)
+
+
+def rcclexchange_from_env(device: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1:
+        return LocalExchange()
+    return RcclExchange(comm_from_env(device), device)

@@ -16,8 +16,8 @@ LIB = os.path.join(HERE, "acmmp", "libacmmp.so")
 ARCH = os.environ.get("ACMMP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["kernels.hip", "capi.cpp", "planar_prior.cpp"]
-HIP_CPP = {"capi.cpp"}              # host C++ that includes HIP headers
+SOURCES = ["kernels.hip", "capi.cpp", "comm.cpp", "planar_prior.cpp"]
+HIP_CPP = {"capi.cpp", "comm.cpp"}              # host C++ that includes HIP headers
 HEADERS = ["engine.h", "detmath.h"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}",
           f"-I{INCLUDE}", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
@@ -45,7 +45,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
                 print("[acmmp build]", " ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)
         objs.append(obj)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs, "-L/opt/rocm/lib", "-lrccl",
+           "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print("[acmmp build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

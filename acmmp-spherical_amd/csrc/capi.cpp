@@ -123,6 +123,7 @@ const char* acmmp_status_str(acmmp_status s) {
     case ACMMP_ERR_STATE: return "call order violated";
     case ACMMP_ERR_UNSUPPORTED: return "unsupported configuration";
     case ACMMP_ERR_NO_DEVICE: return "no HIP device";
+    case ACMMP_ERR_COMM: return "RCCL communicator error";
     }
     return "unknown status";
 }
@@ -285,7 +286,8 @@ acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images,
     return ACMMP_OK;
 }
 
-acmmp_status acmmp_upload_depths(acmmp_ctx* c, int n, const float* const* depths, const int* w, const int* h) {
+static acmmp_status upload_depths(acmmp_ctx* c, int n, const float* const* depths, const int* w, const int* h,
+                                  hipMemcpyKind kind) {
     if (!c || !depths || !w || !h) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
     if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
     if (n < c->N) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "need one depth map per image");
@@ -299,13 +301,30 @@ acmmp_status acmmp_upload_depths(acmmp_ctx* c, int n, const float* const* depths
     }
     HIP_TRY(c, dalloc(c->d_dep, total));
     for (int i = 0; i < c->N; ++i) {
-        HIP_TRY(c, hipMemcpy(c->d_dep + off[i], depths[i], sizeof(float) * w[i] * h[i], hipMemcpyHostToDevice));
+        HIP_TRY(c, hipMemcpy(c->d_dep + off[i], depths[i], sizeof(float) * w[i] * h[i], kind));
         c->dcams[i].dep_off = static_cast<long long>(off[i]);
         c->dcams[i].dep_w = w[i];
         c->dcams[i].dep_h = h[i];
     }
     HIP_TRY(c, hipMemcpy(c->d_cams, c->dcams.data(), sizeof(DevCam) * c->N, hipMemcpyHostToDevice));
     c->has_depths = true;
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_upload_depths(acmmp_ctx* c, int n, const float* const* depths, const int* w, const int* h) {
+    return upload_depths(c, n, depths, w, h, hipMemcpyHostToDevice);
+}
+
+acmmp_status acmmp_upload_depths_device(acmmp_ctx* c, int n, const float* const* depths, const int* w, const int* h) {
+    return upload_depths(c, n, depths, w, h, hipMemcpyDeviceToDevice);
+}
+
+acmmp_status acmmp_export_depth(acmmp_ctx* c, float* dev_dst) {
+    if (!c || !dev_dst) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
+    if (!c->d_planes_rm) return fail(c, ACMMP_ERR_STATE, "no result yet");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, launch_export_depth(c->d_planes_rm, static_cast<long long>(P_of(c)), dev_dst, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     return ACMMP_OK;
 }
 

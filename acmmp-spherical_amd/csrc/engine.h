@@ -108,6 +108,7 @@ hipError_t launch_init(const KParams& kp, hipStream_t s);
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s,
                             hipEvent_t* ev = nullptr);
 hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s);
+hipError_t launch_export_depth(const float4* planes, long long P, float* dst, hipStream_t s);
 hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int sw, int sh, int imagescale,
                       float* out, hipStream_t s);
 hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,

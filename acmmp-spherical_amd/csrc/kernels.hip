@@ -1547,6 +1547,16 @@ hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s) {
     return hipGetLastError();
 }
 
+__global__ void k_export_depth(const float4* __restrict__ planes, long long P, float* __restrict__ dst) {
+    const long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < P) dst[i] = planes[i].w;
+}
+
+hipError_t launch_export_depth(const float4* planes, long long P, float* dst, hipStream_t s) {
+    k_export_depth<<<static_cast<unsigned>((P + 255) / 256), 256, 0, s>>>(planes, P, dst);
+    return hipGetLastError();
+}
+
 hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int sw, int sh, int imagescale,
                       float* out, hipStream_t s) {
     dim3 blk(16, 16), grd(cdiv(W, 16), cdiv(H, 16));

@@ -72,10 +72,13 @@ typedef enum acmmp_status {
     ACMMP_ERR_OUT_OF_MEMORY = 3,
     ACMMP_ERR_STATE = 4,            /* call order violated (e.g. run before upload) */
     ACMMP_ERR_UNSUPPORTED = 5,      /* e.g. mixed camera models, > 32 source views */
-    ACMMP_ERR_NO_DEVICE = 6
+    ACMMP_ERR_NO_DEVICE = 6,
+    ACMMP_ERR_COMM = 7            /* RCCL failure */
 } acmmp_status;
 
 typedef struct acmmp_ctx acmmp_ctx;
+typedef struct acmmp_comm acmmp_comm;
+#define ACMMP_COMM_ID_BYTES 128
 
 /* ACMMP::ACMMP() (ACMMP.cpp:99) + cudaSetDevice (main.cpp:77).  `device` is a HIP
  * ordinal; -1 keeps the calling thread's current device. */
@@ -101,6 +104,15 @@ acmmp_status acmmp_upload_views(acmmp_ctx *ctx, int n, const float *const *image
  * depths[i] is h[i] x w[i] row-major (index 0 = reference, as the reference). */
 acmmp_status acmmp_upload_depths(acmmp_ctx *ctx, int n, const float *const *depths,
                                  const int *w, const int *h);
+
+/* The same from device buffers of this context's GPU (in-memory pipeline: the depth maps a geom
+ * pass reads stay in HBM instead of the reference's depths*.dmb round trip). */
+acmmp_status acmmp_upload_depths_device(acmmp_ctx *ctx, int n, const float *const *dev_depths,
+                                        const int *w, const int *h);
+
+/* The last run's depth map (.w of plane_hypotheses, ProcessProblem main.cpp:103-111) copied into a
+ * device buffer of P floats on this context's GPU. */
+acmmp_status acmmp_export_depth(acmmp_ctx *ctx, float *dev_dst);
 
 /* Reference-view state for geom / hierarchy / planar reuse passes
  * (ACMMP.cpp:772-785, 833-843): planes = P float4 (nx, ny, nz, w) row-major,
@@ -147,6 +159,29 @@ acmmp_status acmmp_last_timing(const acmmp_ctx *ctx, float ms[3]);
  * kernels' stream): summed ms and launch count for [k_eval_nb, k_select, k_eval_ref, k_finish]
  * (the four kernels one CheckerboardPropagation half-sweep is split into). */
 acmmp_status acmmp_last_kernel_timing(const acmmp_ctx *ctx, float ms[4], int launches[4]);
+
+/* ---- device buffers and the multi-GPU communicator (no reference counterpart:
+ * the reference is single-GPU and exchanges depth maps through dmb files) ------------------- */
+
+/* Plain device memory on `device` (pipeline depth store); kind: 0 = H2D, 1 = D2H, 2 = D2D. */
+acmmp_status acmmp_device_alloc(int device, size_t bytes, void **ptr);
+acmmp_status acmmp_device_free(int device, void *ptr);
+acmmp_status acmmp_memcpy(int device, void *dst, const void *src, size_t bytes, int kind);
+
+/* RCCL communicator, one rank per process / GPU.  Rank 0 creates the id and hands the 128 bytes
+ * to the other ranks out of band (the Python driver uses the launcher's TCP store). */
+acmmp_status acmmp_comm_unique_id(uint8_t id[ACMMP_COMM_ID_BYTES]);
+acmmp_status acmmp_comm_create(int device, const uint8_t id[ACMMP_COMM_ID_BYTES], int nranks, int rank,
+                               acmmp_comm **out);
+void acmmp_comm_destroy(acmmp_comm *comm);
+
+/* Grouped in-place broadcasts: device buffer bufs[i] (bytes[i]) from rank roots[i] to every rank.
+ * Synchronous on return. */
+acmmp_status acmmp_comm_broadcast(acmmp_comm *comm, int n, void *const *bufs, const size_t *bytes,
+                                  const int *roots);
+
+/* Element-wise max over ranks of n host doubles (timing reductions); synchronous. */
+acmmp_status acmmp_comm_allreduce_max(acmmp_comm *comm, double *vals, int n);
 
 /* ---- planar-prior host side (no GPU; ACMMP.cpp:904-1011, main.cpp:113-181) ---------------
  * Host restatements of the reference's planar-prior helpers, so a caller can run ProcessProblem's

@@ -1,0 +1,155 @@
+"""Multi-pass pipeline driver: the reference's schedule
+(main.cpp:392-482), ProcessProblem's pass wiring (geom state reload, hierarchy scaled state,
+planar second run, JBU between scales), view sharding over ranks with the depth exchange
+between passes, and -- on the GPU -- the engine-driven pipeline bit-identical to the same
+pipeline driven by the CPU oracle."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from acmmp import io, pipeline
+from conftest import assert_bitwise_equal
+from pipeline_support import GlooExchange, OracleEngine, final_maps, small_dataset
+
+SCHEDULE_2_SCALES = ["planar", "geom", "geom_multi", "hier_planar", "geom", "geom_multi"]
+
+
+def test_resize_linear_matches_closed_form():
+    img = np.arange(12 * 8, dtype=np.float32).reshape(8, 12)        # linear ramp: exact under bilinear
+    out = pipeline.resize_linear(img, 6, 4)
+    # (d + 0.5) * 2 - 0.5 = 2d + 0.5 -> mean of source columns 2d, 2d+1 (and rows)
+    exp = np.array([[(img[2 * r, 2 * c] + img[2 * r, 2 * c + 1] + img[2 * r + 1, 2 * c] + img[2 * r + 1, 2 * c + 1]) / 4
+                     for c in range(6)] for r in range(4)], np.float32)
+    assert np.array_equal(out, exp)
+    up = pipeline.resize_linear(img, 24, 16)
+    assert up[0, 0] == img[0, 0] and up[-1, -1] == img[-1, -1]       # clamped borders
+
+
+def test_scale_view_scales_cameras():
+    ds = small_dataset(64, 32, 2, model="sphere")
+    img, cam = pipeline.scale_view(ds.images[0], ds.cameras[0], 32)
+    assert img.shape == (16, 32) and (cam["width"], cam["height"]) == (32, 16)
+    assert cam["params"][1] == np.float32(ds.cameras[0]["params"][1] * np.float32(0.5))
+    same, cam2 = pipeline.scale_view(ds.images[0], ds.cameras[0], 64)
+    assert same is ds.images[0] and cam2["width"] == 64
+
+
+def test_pipeline_schedule_single_rank():
+    ds = small_dataset(64, 32, 3)
+    pipe = pipeline.Pipeline(ds, engine=OracleEngine(), order="reference", size_bound=40).run()
+    assert [p.name for p in pipe.passes] == SCHEDULE_2_SCALES
+    assert all(p.views == [0, 1, 2] for p in pipe.passes)
+    for v in range(3):
+        d = pipe.store.get("depths_geom", v)
+        assert d.shape == (32, 64)
+        assert np.isfinite(d).mean() > 0.9
+        assert pipe.store.get("normals", v).shape == (32, 64, 3)
+        assert pipe.store.get("depths", v).shape == (32, 64)         # JBU output / hier-planar pass
+
+
+def test_pipeline_writes_reference_layout(tmp_path):
+    ds = small_dataset(48, 24, 2)
+    pipeline.Pipeline(ds, engine=OracleEngine(), order="reference", geom_iterations=1,
+                      out_folder=str(tmp_path)).run()
+    for v in range(2):
+        d = tmp_path / "ACMMP" / f"2333_{v:08d}"
+        for f in ("depths.dmb", "depths_geom.dmb", "normals.dmb", "costs.dmb"):
+            assert (d / f).exists()
+        assert io.read_dmb(str(d / "normals.dmb")).shape == (24, 48, 3)
+
+
+def test_reference_order_differs_from_snapshot_only_in_multi_geometry():
+    """Views of a multi_geometry pass read predecessors' fresh depths_geom in reference order."""
+    ds = small_dataset(48, 24, 3)
+    a = pipeline.Pipeline(ds, engine=OracleEngine(), order="reference", geom_iterations=1).run()
+    b = pipeline.Pipeline(ds, engine=OracleEngine(), order="snapshot", geom_iterations=1).run()
+    ma, mb = final_maps(a), final_maps(b)
+    assert ma.keys() == mb.keys()
+    for k in ma:                                               # one geom pass, no multi_geometry
+        assert_bitwise_equal(ma[k], mb[k], str(k))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank, world, port, outdir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ds = small_dataset(64, 32, 3)
+    pipe = pipeline.Pipeline(ds, engine=OracleEngine(nthreads=2), exchange=GlooExchange(dist), order="snapshot",
+                             size_bound=40).run()
+    maps = final_maps(pipe)
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"),
+             **{f"{k}__{v}": a for (k, v), a in maps.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_snapshot_pipeline_equals_single_rank(tmp_path):
+    """world_size 2 over gloo: views sharded 2 + 1, depth maps exchanged after every pass; the
+    result equals the single-rank snapshot run bit for bit (every view, every stored map)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_rank_main, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    single = final_maps(pipeline.Pipeline(small_dataset(64, 32, 3), engine=OracleEngine(), order="snapshot",
+                                          size_bound=40).run())
+    seen = set()
+    for r in range(2):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        for name in z.files:
+            key, v = name.split("__")
+            v = int(v)
+            owner = v % 2
+            if key in ("normals", "costs") and owner != r:
+                continue
+            assert_bitwise_equal(z[name], single[(key, v)], f"rank {r} {key} view {v}")
+            seen.add((key, v))
+    assert {(k, v) for (k, v) in single} <= seen
+
+
+@pytest.mark.gpu
+def test_gpu_pipeline_bitexact_vs_oracle_pipeline():
+    ds = small_dataset(64, 32, 3)
+    gpu = pipeline.Pipeline(ds, order="reference", size_bound=40).run()
+    cpu = pipeline.Pipeline(ds, engine=OracleEngine(), order="reference", size_bound=40).run()
+    mg, mc = final_maps(gpu), final_maps(cpu)
+    assert mg.keys() == mc.keys() and len(mg) >= 12
+    for k in mc:
+        assert_bitwise_equal(mg[k], mc[k], str(k))
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank_comm_and_device_store():
+    """The RCCL communicator and device buffers of the exchange path on one rank (multi-rank runs
+    need one GPU per rank: RCCL refuses two ranks on one device)."""
+    from acmmp import capi
+    comm = capi.Comm(0, capi.Comm.unique_id(), 1, 0)
+    a = np.random.default_rng(0).normal(size=(17, 33)).astype(np.float32)
+    buf = capi.DeviceBuffer(0, a.shape)
+    buf.upload(a)
+    comm.broadcast([buf], [0])
+    assert np.array_equal(buf.download(), a)
+    assert np.array_equal(comm.allreduce_max([1.5, -2.0]), [1.5, -2.0])
+    comm.close()
+    buf.free()
+
+
+@pytest.mark.gpu
+def test_gpu_export_and_device_depth_upload_roundtrip():
+    from acmmp import capi
+    ds = small_dataset(48, 24, 2)
+    pipe = pipeline.Pipeline(ds, order="reference", geom_iterations=1)
+    assert pipe.store.device is not None
+    pipe.run()
+    for v in range(2):
+        host = pipe.store.get("depths_geom", v)
+        dev = pipe.store.dev[("depths_geom", v)].download()
+        assert_bitwise_equal(dev, host, f"view {v}")
+    assert isinstance(pipe.engine, capi.Context)
