@@ -432,3 +432,55 @@ def rcclexchange_from_env(device: int):
     if world == 1:
         return LocalExchange()
     return RcclExchange(comm_from_env(device), device)
+
+
+def write_dense_folder(folder: str, ds: Dataset, pairs=None, quality: int = 95):
+    """Synthetic dataset -> the reference's dense-folder layout (images/%08d.jpg, cams/%08d_cam.txt,
+    pair.txt).  PINHOLE depth lines carry `dmin dmax N dmax`, so the reader quirk (ACMMP.cpp:205:
+    second token -> depth_max) yields the intended range."""
+    from PIL import Image
+    os.makedirs(os.path.join(folder, "images"), exist_ok=True)
+    os.makedirs(os.path.join(folder, "cams"), exist_ok=True)
+    for i, img in ds.images.items():
+        Image.fromarray(np.clip(np.round(img), 0, 255).astype(np.uint8), "L").save(
+            os.path.join(folder, "images", f"{i:08d}.jpg"), quality=quality)
+        cam = ds.cameras[i]
+        interval = float(cam["depth_max"]) if int(cam["model"]) == types.PINHOLE else 0.0
+        io.write_camera(os.path.join(folder, "cams", f"{i:08d}_cam.txt"), cam, depth_interval=interval)
+    if pairs is None:
+        pairs = [(p.ref_image_id, [(s, 1.0) for s in p.src_image_ids]) for p in ds.problems]
+    io.write_pair_list(folder, pairs)
+
+
+def main(argv=None):
+    """`python -m acmmp.pipeline DENSE_FOLDER` -- the reference's `ACMMP dense_folder` without fusion.
+    Under torchrun (WORLD_SIZE > 1) every rank drives GPU LOCAL_RANK, views are sharded and the
+    depth maps are exchanged over RCCL between passes (snapshot order)."""
+    import argparse
+    import json
+    import time
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dense_folder")
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--order", choices=["reference", "snapshot"], default=None)
+    ap.add_argument("--geom-iterations", type=int, default=2)
+    ap.add_argument("--no-dmb", action="store_true", help="keep results in memory only")
+    a = ap.parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    device = int(os.environ.get("LOCAL_RANK", "0"))
+    order = a.order or ("reference" if world == 1 else "snapshot")
+    ds = load_dataset(a.dense_folder)
+    exchange = rcclexchange_from_env(device)
+    t0 = time.perf_counter()
+    pipe = Pipeline(ds, exchange=exchange, device=device, seed=a.seed, order=order,
+                    geom_iterations=a.geom_iterations, out_folder=None if a.no_dmb else a.dense_folder,
+                    log=lambda *m: print(*m, flush=True)).run()
+    dt = time.perf_counter() - t0
+    print(json.dumps({"rank": pipe.rank, "world": pipe.world, "views": len(pipe.my_problems()),
+                      "passes": [p.name for p in pipe.passes], "seconds": round(dt, 3)}), flush=True)
+    exchange.close()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

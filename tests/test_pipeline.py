@@ -153,3 +153,20 @@ def test_gpu_export_and_device_depth_upload_roundtrip():
         dev = pipe.store.dev[("depths_geom", v)].download()
         assert_bitwise_equal(dev, host, f"view {v}")
     assert isinstance(pipe.engine, capi.Context)
+
+
+def test_dense_folder_roundtrip(tmp_path):
+    """write_dense_folder -> load_dataset: the reference's on-disk layout, pinhole reader quirk
+    handled by the writer, JPEG luma decoded back within quantisation."""
+    ds = small_dataset(48, 32, 3, model="pinhole")
+    pipeline.write_dense_folder(str(tmp_path), ds, quality=100)
+    back = pipeline.load_dataset(str(tmp_path))
+    assert [p.ref_image_id for p in back.problems] == [0, 1, 2]
+    assert back.problems[1].src_image_ids == [0, 2]
+    for i in range(3):
+        assert back.images[i].shape == ds.images[i].shape
+        assert np.abs(back.images[i] - np.round(ds.images[i])).max() <= 3
+        c, d = back.cameras[i], ds.cameras[i]
+        assert np.allclose(c["K"], d["K"]) and np.allclose(c["R"], d["R"]) and np.allclose(c["t"], d["t"])
+        assert c["depth_min"] == d["depth_min"] and c["depth_max"] == d["depth_max"]
+        assert (c["width"], c["height"]) == (48, 32)
