@@ -218,6 +218,7 @@ __device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_read
 struct Patch {
     const float4* rw;               // [s * stride] = (ray.x, ray.y, ray.z, w); null when not staged
     const float* rr;                // [s * stride] = reference texel
+    const float2* wr;               // lite staging: [s * stride] = (w, texel); rays re-read from the tables
     int stride;
     float center;                   // reference texel at the pixel
     float sbw, sref, srr;
@@ -243,13 +244,21 @@ __device__ __forceinline__ float bilinear_pair(const float* img, int pitch, int 
 }
 
 // The same fetch through a buffer descriptor of the view's padded image (32-bit texel offsets,
-// 24-bit multiply).  SPHERE callers pass x already wrapped and y clamped to [0, H-1] (never NaN),
-// so y needs no clamp; x keeps clampi(f2i_sat(floor x), -1, W-1): the float clamp below is the
-// same map for every non-NaN value, and NaN -> 0 as f2i_sat does.
+// 24-bit multiply), split into issue (Tap) and use (lerp_tap) so a caller can put the loads of
+// several views in flight before consuming any.  SPHERE callers pass x already wrapped and y
+// clamped to [0, H-1] (never NaN), so y needs no clamp; x keeps clampi(f2i_sat(floor x), -1, W-1):
+// the float clamp below is the same map for every non-NaN value, and NaN -> 0 as f2i_sat does.
+struct Tap {
+    float a, b;
+    f32x2 top, bot;
+};
+
 template <bool Y_IN_RANGE>
-__device__ __forceinline__ float bilinear_rsrc(__amdgpu_buffer_rsrc_t rs, int pitch, int W, int H, float x, float y) {
+__device__ __forceinline__ Tap fetch_tap(__amdgpu_buffer_rsrc_t rs, int pitch, int W, int H, float x, float y) {
     const float fx = floorf(x), fy = floorf(y);
-    const float a = x - fx, b = y - fy;
+    Tap t;
+    t.a = x - fx;
+    t.b = y - fy;
     int ix = static_cast<int>(fminf(fmaxf(fx, -1.0f), static_cast<float>(W - 1)));
     ix = fx != fx ? 0 : ix;
     int iy;
@@ -260,11 +269,15 @@ __device__ __forceinline__ float bilinear_rsrc(__amdgpu_buffer_rsrc_t rs, int pi
         iy = fy != fy ? 0 : iy;
     }
     const int off = (__mul24(iy + 1, pitch) + ix + 1) * 4;
-    const f32x2 top = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
-    const f32x2 bot = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, pitch * 4, 0));
-    const float r0 = fmaf(a, top.y - top.x, top.x);
-    const float r1 = fmaf(a, bot.y - bot.x, bot.x);
-    return fmaf(b, r1 - r0, r0);
+    t.top = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+    t.bot = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, pitch * 4, 0));
+    return t;
+}
+
+__device__ __forceinline__ float lerp_tap(const Tap& t) {
+    const float r0 = fmaf(t.a, t.top.y - t.top.x, t.top.x);
+    const float r1 = fmaf(t.a, t.bot.y - t.bot.x, t.bot.x);
+    return fmaf(t.b, r1 - r0, r0);
 }
 
 // Sample s = (i, j) of pixel (px, py): ray, bilateral weight and reference texel.
@@ -298,6 +311,9 @@ __device__ __forceinline__ void patch_sums(const KParams& kp, Patch& pt, int px 
             if (pt.rw) {
                 w = pt.rw[s * pt.stride].w;
                 r = pt.rr[s * pt.stride];
+            } else if (pt.wr) {
+                w = pt.wr[s * pt.stride].x;
+                r = pt.wr[s * pt.stride].y;
             } else {
                 w = patch_sample<MODEL>(kp, px, py, s, -kp.R + (s / kp.nside) * kp.inc,
                                         -kp.R + (s % kp.nside) * kp.inc, pt.center, r).w;
@@ -315,7 +331,7 @@ template <int MODEL>
 __device__ __forceinline__ Patch make_patch(const KParams& kp, int px, int py) {
     const DevCam& rc = kp.cams[0];
     Patch pt;
-    pt.rw = nullptr; pt.rr = nullptr; pt.stride = 0;
+    pt.rw = nullptr; pt.rr = nullptr; pt.wr = nullptr; pt.stride = 0;
     pt.center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
     patch_sums<MODEL>(kp, pt, px, py);
     return pt;
@@ -366,7 +382,9 @@ __device__ __forceinline__ void project_pc(const ProjCam& c, float3 P, float& ox
 
 // ComputeBilateralNCC (ACMMP.cu:405-516) of plane `ph` at pixel (px, py) against the
 // source views vlist[0..nv) (wave-uniform camera indices 1..N-1), sample-outer.
-template <int MODEL, int VB, bool STAGED>
+// STAGED: 0 = samples recomputed here, 1 = (ray, w) + texel staged in LDS, 2 = (w, texel) staged
+// and the ray re-read from the ray tables (less LDS per pixel, more blocks per CU).
+template <int MODEL, int VB, int STAGED, bool PIPE>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv, float (&cost)[VB]) {
     const DevCam& rc = kp.cams[0];
@@ -399,44 +417,66 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
         for (int j = -R; j <= R; j += inc, ++s) {
             float r;
             float4 rw;
-            if (STAGED) {
+            if (STAGED == 1) {
                 rw = pt.rw[s * pt.stride];
                 r = pt.rr[s * pt.stride];
+            } else if (STAGED == 2) {
+                const float2 q = pt.wr[s * pt.stride];
+                rw = ray_at<MODEL>(kp, px + i, py + j);
+                rw.w = q.x;
+                r = q.y;
             } else {
                 rw = patch_sample<MODEL>(kp, px, py, s, i, j, pt.center, r);
             }
             const float w = rw.w;
             const float3 P = world_point_ray<MODEL>(rc, px + i, py + j, depth_from_plane(ph, rw), rw);
             const float wr = w * r;
+            Tap tap[VB];
+            bool ok[VB];
+            // accumulate view v's sample (ACMMP.cu:488-498)
+#define ACMMP_ACCUMULATE(v)                                                  \
+            do {                                                             \
+                const float sp = lerp_tap(tap[v]);                           \
+                if (ok[v]) {                                                 \
+                    if (MODEL == kPinhole) {                                 \
+                        sbw[v] += w;                                         \
+                        sref[v] = fmaf(w, r, sref[v]);                       \
+                        srr[v] = fmaf(wr, r, srr[v]);                        \
+                    }                                                        \
+                    ssrc[v] = fmaf(w, sp, ssrc[v]);                          \
+                    const float ws = w * sp;                                 \
+                    sss[v] = fmaf(ws, sp, sss[v]);                           \
+                    srs[v] = fmaf(wr, sp, srs[v]);                           \
+                }                                                            \
+            } while (0)
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
+                ok[v] = false;
                 if (v < nv) {
                     ConstCam& c = PCV(v);
                     float sx, sy, sd;
                     project<MODEL>(c, P, sx, sy, sd);
-                    bool ok = true;
+                    ok[v] = true;
                     if (MODEL == kSphere) {
                         sx = fmaf(-floorf(sx * c.invW), c.Wf, sx);
                         sy = fminf(fmaxf(sy, 0.0f), c.Hf - 1.0f);
                     } else {
-                        ok = !(sx < 0.0f || sx >= c.Wf || sy < 0.0f || sy >= c.Hf);
+                        ok[v] = !(sx < 0.0f || sx >= c.Wf || sy < 0.0f || sy >= c.Hf);
                     }
                     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                         const_cast<float*>(kp.img + c.img_off), 0, c.img_bytes, 0x00020000);
-                    const float sp = bilinear_rsrc<MODEL == kSphere>(rs, c.img_pitch, c.W, c.H, sx, sy);
-                    if (ok) {
-                        if (MODEL == kPinhole) {
-                            sbw[v] += w;
-                            sref[v] = fmaf(w, r, sref[v]);
-                            srr[v] = fmaf(wr, r, srr[v]);
-                        }
-                        ssrc[v] = fmaf(w, sp, ssrc[v]);
-                        const float ws = w * sp;
-                        sss[v] = fmaf(ws, sp, sss[v]);
-                        srs[v] = fmaf(wr, sp, srs[v]);
-                    }
+                    tap[v] = fetch_tap<MODEL == kSphere>(rs, c.img_pitch, c.W, c.H, sx, sy);
+                    if (!PIPE) ACMMP_ACCUMULATE(v);
                 }
             }
+            // PIPE: every view's texels are in flight before the first is used (more latency
+            // hidden per wave, ~6 more VGPRs per view)
+            if (PIPE) {
+#pragma unroll
+                for (int v = 0; v < VB; ++v)
+                    if (v < nv) ACMMP_ACCUMULATE(v);
+            }
+#undef ACMMP_ACCUMULATE
         }
     }
 #pragma unroll
@@ -543,7 +583,7 @@ __device__ __forceinline__ float4 perturbed_normal(float4 v, float4 n, Rng& rs, 
 // ------------------------------------------------------------------ cost-vector helpers
 
 // Evaluate all source views of plane `ph` and hand each cost to f(view0, cost) in view order.
-template <int MODEL, int VB, bool STAGED, typename F>
+template <int MODEL, int VB, int STAGED, bool PIPE, typename F>
 __device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                               uint32_t wave_mask, F&& f) {
     int v = 0;
@@ -565,7 +605,7 @@ __device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py,
         }
         if (nv == 0) break;
         float cost[VB];
-        ncc_chunk<MODEL, VB, STAGED>(kp, px, py, pt, ph, vlist, nv, cost);
+        ncc_chunk<MODEL, VB, STAGED, PIPE>(kp, px, py, pt, ph, vlist, nv, cost);
 #pragma unroll
         for (int k = 0; k < VB; ++k)
             if (k < nv) f(vlist[k] - 1, cost[k]);
@@ -658,7 +698,7 @@ __device__ float initial_cost(const KParams& kp, int px, int py, const Patch& pt
     float cv[kMaxViews], cvc[kMaxViews];
     int nvalid = 0;
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
-    for_all_views<MODEL, VB, false>(kp, px, py, pt, ph, all, [&](int v, float c) {
+    for_all_views<MODEL, VB, 0, true>(kp, px, py, pt, ph, all, [&](int v, float c) {
         cv[v] = c;
         cvc[v] = c;
         if (c < 2.0f) nvalid++;
@@ -921,10 +961,34 @@ __device__ __forceinline__ Patch coop_patch(const KParams& kp, bool valid, int p
     }
     __syncthreads();
     Patch pt;
-    pt.rw = rw; pt.rr = rr; pt.stride = 1;
+    pt.rw = rw; pt.rr = rr; pt.wr = nullptr; pt.stride = 1;
     pt.center = 0.f;
     // every lane of the pixel sums its SPHERE weights itself (same order, same bits): no LDS slot
     // and no second barrier, which keeps k_eval_nb's block at 20160 B of LDS (8 blocks per CU)
+    if (valid) patch_sums<MODEL>(kp, pt);
+    else { pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f; }
+    return pt;
+}
+
+// Lite staging: only (w, texel) per sample in LDS (8 B instead of 20 B).
+template <int MODEL>
+__device__ __forceinline__ Patch coop_patch_lite(const KParams& kp, bool valid, int px, int py, int lp, int h,
+                                                 int nh, float2* lwr) {
+    float2* wr = lwr + lp * kp.S;
+    if (valid) {
+        const DevCam& rc = kp.cams[0];
+        const float center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
+        for (int s = h; s < kp.S; s += nh) {
+            const int i = -kp.R + (s / kp.nside) * kp.inc, j = -kp.R + (s % kp.nside) * kp.inc;
+            float r;
+            const float w = patch_sample<MODEL>(kp, px, py, s, i, j, center, r).w;
+            wr[s] = make_float2(w, r);
+        }
+    }
+    __syncthreads();
+    Patch pt;
+    pt.rw = nullptr; pt.rr = nullptr; pt.wr = wr; pt.stride = 1;
+    pt.center = 0.f;
     if (valid) patch_sums<MODEL>(kp, pt);
     else { pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f; }
     return pt;
@@ -960,7 +1024,7 @@ __global__ __launch_bounds__(256) void k_eval_nb(const KParams kp, const int col
     }
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
-    for_all_views<MODEL, VB, true>(kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
+    for_all_views<MODEL, VB, 1, false>(kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
 }
 
 // Joint view selection, aggregation, acceptance and refinement candidates (ACMMP.cu:1146-1311,
@@ -1242,9 +1306,7 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
 template <int MODEL, int VB>
 __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int colour) {
-    extern __shared__ float4 lds4[];
-    float4* lrw = lds4;
-    float* lrr = reinterpret_cast<float*>(lds4 + kRefPix * kp.S);
+    extern __shared__ float2 lds2[];
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
     const long long q = static_cast<long long>(blockIdx.x) * kRefPix + lp;
@@ -1260,7 +1322,7 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
         vw = st.vw;
         weight_norm = st.weight_norm;
     }
-    const Patch pt = coop_patch<MODEL>(kp, valid, px, py, lp, h, kRefLanes, lrw, lrr);
+    const Patch pt = coop_patch_lite<MODEL>(kp, valid, px, py, lp, h, kRefLanes, lds2);
     if (!valid) return;
     const float4 dc = ray_at<MODEL>(kp, px, py);
     const float4 tp = kp.cand[h * Pc + ci];
@@ -1270,7 +1332,7 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
     uint32_t mask = 0u;
     for (int v = 0; v < kp.V; ++v) if (vw_get(vwp, v) > 0.0f) mask |= 1u << v;
     float temp_cost = 0.0f;
-    for_all_views<MODEL, VB, true>(kp, px, py, pt, tp, wave_or(mask, kp.V), [&](int v, float c) {
+    for_all_views<MODEL, VB, 2, true>(kp, px, py, pt, tp, wave_or(mask, kp.V), [&](int v, float c) {
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
             if (kp.geom) temp_cost = fmaf(w, fmaf(0.1f, geom_cost<MODEL>(kp, v + 1, tp, px, py, dc), c), temp_cost);
@@ -1448,7 +1510,7 @@ __global__ void k_debug(const KParams kp, int which, int n, const int* __restric
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     if (which == 0) {
         const Patch pt = make_patch<MODEL>(kp, x, y);
-        for_all_views<MODEL, VB, false>(kp, x, y, pt, ph, all,
+        for_all_views<MODEL, VB, 0, true>(kp, x, y, pt, ph, all,
                                  [&](int v, float c) { out[static_cast<long long>(q) * kp.V + v] = c; });
     } else {
         const float4 dc = ray_at<MODEL>(kp, x, y);
@@ -1515,7 +1577,7 @@ hipError_t launch_init(const KParams& kp, hipStream_t s) {
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s, hipEvent_t* ev) {
     const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
     const size_t lds_nb = (sizeof(float4) + sizeof(float)) * kNbPix * kp.S;
-    const size_t lds_ref = (sizeof(float4) + sizeof(float)) * kRefPix * kp.S;
+    const size_t lds_ref = sizeof(float2) * kRefPix * kp.S;
     hipError_t e = hipSuccess;
 #define ACMMP_MARK(i) if (ev && (e = hipEventRecord(ev[i], s)) != hipSuccess) return e
     ACMMP_MARK(0);
