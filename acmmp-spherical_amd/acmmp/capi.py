@@ -14,7 +14,8 @@ import numpy as np
 from .types import CAMERA_DTYPE, PARAMS_DTYPE
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libacmmp.so")
+# ACMMP_LIB selects another in-tree build of the same library (A/B experiments); default: the product build
+LIB_PATH = os.environ.get("ACMMP_LIB") or os.path.join(HERE, "libacmmp.so")
 
 STATUS = {0: "ok", 1: "invalid argument", 2: "HIP runtime error", 3: "out of device memory",
           4: "call order violated", 5: "unsupported configuration", 6: "no HIP device"}

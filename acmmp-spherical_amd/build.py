@@ -27,11 +27,13 @@ def _newest(paths):
     return max(os.path.getmtime(p) for p in paths)
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
+def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines=(), objdir: str | None = None) -> str:
+    """Compile csrc/ into `lib`.  `defines` (e.g. ["ACMMP_EXPERIMENT=1"]) + a separate `objdir` give an
+    experiment variant next to the product build (select it at run time with ACMMP_LIB=<path>)."""
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(INCLUDE, "acmmp.h")]
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest(deps):
-        return LIB
-    objdir = os.path.join(HERE, "build")
+    if not force and os.path.exists(lib) and os.path.getmtime(lib) >= _newest(deps):
+        return lib
+    objdir = objdir or os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
     objs = []
     for src in SOURCES:
@@ -40,17 +42,17 @@ def build(force: bool = False, verbose: bool = True) -> str:
         hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "acmmp.h")]
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < _newest([srcp] + hdrs):
             lang = ["-x", "hip"] if src in HIP_CPP else []
-            cmd = [HIPCC, *COMMON, *lang, "-c", srcp, "-o", obj]
+            cmd = [HIPCC, *COMMON, *[f"-D{d}" for d in defines], *lang, "-c", srcp, "-o", obj]
             if verbose:
                 print("[acmmp build]", " ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)
         objs.append(obj)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs, "-L/opt/rocm/lib", "-lrccl",
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs, "-L/opt/rocm/lib", "-lrccl",
            "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print("[acmmp build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

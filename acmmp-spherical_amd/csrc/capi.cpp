@@ -412,17 +412,19 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     HIP_TRY(c, dalloc(c->d_spatial, static_cast<size_t>(c->model == kSphere ? c->H : 1) * kp.S));
     HIP_TRY(c, launch_spatial_table(kp, c->d_spatial, c->stream));
     // half-sweep scratch slab: carve the pieces of engine.h's KParams out of one allocation
-    size_t off[7];
+    size_t off[10];
     {
-        const size_t sizes[6] = {sizeof(float) * 9 * static_cast<size_t>(kp.V) * Pc, sizeof(int) * 8 * Pc,
+        const size_t VP = static_cast<size_t>(kp.V) * Pc;
+        const size_t sizes[9] = {sizeof(float) * 8 * VP, sizeof(int) * 8 * Pc,
                                  sizeof(float4) * 5 * Pc, sizeof(float) * 5 * Pc, sizeof(float) * 5 * Pc,
-                                 sizeof(PixState) * Pc};
+                                 sizeof(PixState) * Pc, sizeof(float) * VP, sizeof(float) * VP,
+                                 sizeof(float) * 5 * VP};
         off[0] = 0;
-        for (int k = 0; k < 6; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
+        for (int k = 0; k < 9; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
     }
-    if (c->scratch_bytes < off[6]) {
-        HIP_TRY(c, dalloc(c->d_scratch, off[6]));
-        c->scratch_bytes = off[6];
+    if (c->scratch_bytes < off[9]) {
+        HIP_TRY(c, dalloc(c->d_scratch, off[9]));
+        c->scratch_bytes = off[9];
     }
     kp.cams = c->d_cams;
     kp.img = c->d_img;
@@ -445,6 +447,9 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.cand_dep = reinterpret_cast<float*>(c->d_scratch + off[3]);
     kp.cand_cost = reinterpret_cast<float*>(c->d_scratch + off[4]);
     kp.pst = reinterpret_cast<PixState*>(c->d_scratch + off[5]);
+    kp.cvec[0] = reinterpret_cast<float*>(c->d_scratch + off[6]);
+    kp.cvec[1] = reinterpret_cast<float*>(c->d_scratch + off[7]);
+    kp.cand_vcost = reinterpret_cast<float*>(c->d_scratch + off[8]);
     return ACMMP_OK;
 }
 

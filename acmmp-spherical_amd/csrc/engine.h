@@ -50,7 +50,8 @@ struct PixState {
     float cost_now, depth_now, cur_cost, restricted_cost;
     uint32_t cur_sel, flags;        // flags: 1 = prior restricted, 2 = refinement runs
     float weight_norm;
-    uint32_t pad;
+    uint32_t src;                   // hypothesis ids of plane_now (bits 0-7) and cur_plane (8-15):
+                                    // 0-7 neighbour direction, 8 current plane, 9+k candidate k
 };
 
 struct KParams {
@@ -85,7 +86,10 @@ struct KParams {
     uint32_t* sel_cs[2];
     uint32_t* rng_cs[2];            // Philox draw counter per pixel
     // half-sweep scratch slab (one colour at a time)
-    float* hyp_cost;                // [9][V][Pc] cost vectors of the 8 neighbours + current plane
+    float* hyp_cost;                // [8][V][Pc] cost vectors of the 8 neighbour hypotheses
+    float* cvec[2];                 // per colour [V][Pc]: NCC cost vector of the pixel's current plane
+                                    // (NaN = view not evaluated for it yet)
+    float* cand_vcost;              // [5][V][Pc] refinement candidates' cost vectors (NaN = not evaluated)
     int* nbpos;                     // [8][Pc] picked neighbour (x | y << 16) or -1
     float4* cand;                   // [5][Pc] refinement candidate planes
     float* cand_dep;                // [5][Pc] their depths (prior term, ACMMP.cu:912)

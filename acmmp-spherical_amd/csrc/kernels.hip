@@ -383,7 +383,8 @@ __device__ __forceinline__ void project_pc(const ProjCam& c, float3 P, float& ox
 // ComputeBilateralNCC (ACMMP.cu:405-516) of plane `ph` at pixel (px, py) against the
 // source views vlist[0..nv) (wave-uniform camera indices 1..N-1), sample-outer.
 // STAGED: 0 = samples recomputed here, 1 = (ray, w) + texel staged in LDS, 2 = (w, texel) staged
-// and the ray re-read from the ray tables (less LDS per pixel, more blocks per CU).
+// and the ray re-read from the ray tables (less LDS per pixel, more blocks per CU), 3 = the
+// k_eval_nb layout of coop_patch_nb.
 template <int MODEL, int VB, int STAGED, bool PIPE>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv, float (&cost)[VB]) {
@@ -420,6 +421,15 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             if (STAGED == 1) {
                 rw = pt.rw[s * pt.stride];
                 r = pt.rr[s * pt.stride];
+            } else if (STAGED == 3) {                    // coop_patch_nb layout
+                const float4 q = pt.rw[s];
+                if (MODEL == kSphere) {
+                    rw = make_float4(q.x, pt.rr[s % kp.nside], q.y, q.z);
+                    r = q.w;
+                } else {
+                    rw = q;
+                    r = pt.rr[s];
+                }
             } else if (STAGED == 2) {
                 const float2 q = pt.wr[s * pt.stride];
                 rw = ray_at<MODEL>(kp, px + i, py + j);
@@ -694,8 +704,10 @@ __device__ __forceinline__ void sort_small(float* d, int n) {
 
 // ComputeMultiViewInitialCostandSelectedViews, ACMMP.cu:519-556
 template <int MODEL, int VB>
-__device__ float initial_cost(const KParams& kp, int px, int py, const Patch& pt, float4 ph, uint32_t* sel) {
-    float cv[kMaxViews], cvc[kMaxViews];
+__device__ float initial_cost(const KParams& kp, int px, int py, const Patch& pt, float4 ph, uint32_t* sel,
+                              float* cvec = nullptr) {
+    constexpr int VMAX = VB < 8 ? VB : kMaxViews;            // pick_vb: V <= VB when VB < 8
+    float cv[VMAX], cvc[VMAX];
     int nvalid = 0;
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     for_all_views<MODEL, VB, 0, true>(kp, px, py, pt, ph, all, [&](int v, float c) {
@@ -703,6 +715,8 @@ __device__ float initial_cost(const KParams& kp, int px, int py, const Patch& pt
         cvc[v] = c;
         if (c < 2.0f) nvalid++;
     });
+    if (cvec)                                                   // current-plane cost cache
+        for (int v = 0; v < kp.V; ++v) cvec[v * kp.Pc] = cvc[v];
     sort_small(cv, kp.V);
     *sel = 0;
     const int top_k = nvalid < kp.top_k ? nvalid : kp.top_k;
@@ -731,7 +745,11 @@ __device__ __forceinline__ float range_gauss(float x, float sigma) {
 // ------------------------------------------------------------------ kernel: RandomInitialization
 
 // ACMMP.cu:673-795.  Reads the persistent row-major state, writes the colour-split working state.
-template <int MODEL, int VB>
+// RandomInitialization branch, uniform over a launch (ACMMP.cu:686-793): one kernel per branch so
+// the common random branch does not carry the JBU loop's registers.
+enum InitBranch { kInitRandom = 0, kInitPlanar = 1, kInitUpsample = 2, kInitReuse = 3 };
+
+template <int MODEL, int VB, int BR>
 __global__ __launch_bounds__(256) void k_init(const KParams kp) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y * blockDim.y + threadIdx.y;
@@ -741,18 +759,19 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
     const int colour = (x + y) & 1;
     const long long ci = cs_index(kp, x, y);
     const Patch pt = make_patch<MODEL>(kp, x, y);
+    float* cvec = kp.cvec[colour] + ci;
     Rng rs;
     rs.init(kp.seed_lo, kp.seed_hi, static_cast<uint32_t>(center), 0u);
     const float4 dc = ray_at<MODEL>(kp, x, y);
     float4 ph;
     float cost;
     uint32_t sel = 0;
-    if (!kp.geom && !kp.hier) {
+    if (BR == kInitRandom) {
         const float depth = fmaf(rs.uniform(), kp.depth_max - kp.depth_min, kp.depth_min);
         ph = random_normal(dc, rs);
         ph.w = dist_to_origin(dc, depth, ph);
-        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel);
-    } else if (kp.planar) {
+        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel, cvec);
+    } else if (BR == kInitPlanar) {
         if (kp.mask[center] > 0 && kp.costs_rm[center] >= 0.1f) {
             const float perturbation = 0.02f;
             const float4 prior = kp.prior[center];
@@ -767,8 +786,8 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
             const float depth = ph.w;
             ph.w = dist_to_origin(dc, depth, ph);
         }
-        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel);
-    } else if (kp.upsample) {
+        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel, cvec);
+    } else if (BR == kInitUpsample) {
         const float scale = static_cast<float>(1.0 * static_cast<double>(kp.scaled_cols) / static_cast<double>(kp.W));
         const float sigmad = 0.50f, sigmar = 25.5f;
         const int Imagescale = f2i_sat(fmaxf(static_cast<float>(kp.W) / kp.scaled_cols,
@@ -804,13 +823,13 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
         kp.pre_rm[center] = initial_cost<MODEL, VB>(kp, x, y, pt, cur, &sel0);
         ph = to_ref(rc, make_float4(nx, ny, nz, 0.0f));
         ph.w = dist_to_origin(dc, cur.w, ph);
-        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel);
+        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel, cvec);
     } else {
         ph = kp.hier ? kp.scaled[center] : kp.planes_rm[center];
         ph = to_ref(rc, ph);
         const float depth = ph.w;
         ph.w = dist_to_origin(dc, depth, ph);
-        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel);
+        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel, cvec);
     }
     kp.plane_cs[colour][ci] = ph;
     kp.cost_cs[colour][ci] = cost;
@@ -970,6 +989,56 @@ __device__ __forceinline__ Patch coop_patch(const KParams& kp, bool valid, int p
     return pt;
 }
 
+// k_eval_nb staging, 16 B per sample + 4 B per patch row: SPHERE stores (ray.x, ray.z, w, texel)
+// per sample and ray.y = -sin(lat) once per patch row (it depends on the row only); PINHOLE stores
+// (ray, w) per sample and the texels after them.  32 pixels x 36 samples = 19.2 KB per block for
+// SPHERE (8 blocks per CU).
+constexpr int kNbLanes = 8;                 // the 8 neighbour directions (the current plane's costs are cached)
+constexpr int kNbPix = 32;                  // pixels per 256-lane block
+
+static inline size_t nb_lds_bytes(int model, int S, int nside) {
+    return model == kSphere ? (sizeof(float4) * S + sizeof(float) * nside) * kNbPix
+                            : (sizeof(float4) + sizeof(float)) * S * kNbPix;
+}
+
+template <int MODEL>
+__device__ __forceinline__ Patch coop_patch_nb(const KParams& kp, bool valid, int px, int py, int lp, int h,
+                                               float4* lds) {
+    float4* rw = lds + lp * kp.S;
+    float* tail = reinterpret_cast<float*>(lds + kNbPix * kp.S);
+    float* rr = tail + lp * (MODEL == kSphere ? kp.nside : kp.S);
+    if (valid) {
+        const DevCam& rc = kp.cams[0];
+        const float center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
+        for (int s = h; s < kp.S; s += kNbLanes) {
+            const int i = -kp.R + (s / kp.nside) * kp.inc, j = -kp.R + (s % kp.nside) * kp.inc;
+            float r;
+            const float4 q = patch_sample<MODEL>(kp, px, py, s, i, j, center, r);
+            if (MODEL == kSphere) {
+                rw[s] = make_float4(q.x, q.z, q.w, r);
+                if (s < kp.nside) rr[s] = q.y;          // samples 0..nside-1 cover every patch row j
+            } else {
+                rw[s] = q;
+                rr[s] = r;
+            }
+        }
+    }
+    __syncthreads();
+    Patch pt;
+    pt.rw = rw; pt.rr = rr; pt.wr = nullptr; pt.stride = 1;
+    pt.center = 0.f;
+    pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f;
+    if (MODEL == kSphere && valid) {
+        for (int s = 0; s < kp.S; ++s) {                // patch_sums order (ACMMP.cu:482-486)
+            const float w = rw[s].z, r = rw[s].w;
+            pt.sbw += w;
+            pt.sref = fmaf(w, r, pt.sref);
+            pt.srr = fmaf(w * r, r, pt.srr);
+        }
+    }
+    return pt;
+}
+
 // Lite staging: only (w, texel) per sample in LDS (8 B instead of 20 B).
 template <int MODEL>
 __device__ __forceinline__ Patch coop_patch_lite(const KParams& kp, bool valid, int px, int py, int lp, int h,
@@ -994,42 +1063,33 @@ __device__ __forceinline__ Patch coop_patch_lite(const KParams& kp, bool valid, 
     return pt;
 }
 
-constexpr int kNbLanes = 9;                 // 8 neighbour directions + the current plane
-constexpr int kNbPix = 28;                  // pixels per 256-lane block (252 lanes used)
 constexpr int kRefLanes = 5;                // refinement candidates (ACMMP.cu:870)
 constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 lanes used)
 
 template <int MODEL, int VB>
-__global__ __launch_bounds__(256) void k_eval_nb(const KParams kp, const int colour) {
+__global__ __launch_bounds__(256, 8) void k_eval_nb(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
-    float4* lrw = lds4;
-    float* lrr = reinterpret_cast<float*>(lds4 + kNbPix * kp.S);
     const int t = threadIdx.x;
     const int lp = t / kNbLanes, h = t - lp * kNbLanes;
     const long long q = static_cast<long long>(blockIdx.x) * kNbPix + lp;
     int px = 0, py = 0;
-    const bool valid = t < kNbPix * kNbLanes && colour_pixel(kp, colour, q, px, py);
-    const Patch pt = coop_patch<MODEL>(kp, valid, px, py, lp, h, kNbLanes, lrw, lrr);
+    const bool valid = colour_pixel(kp, colour, q, px, py);
+    const Patch pt = coop_patch_nb<MODEL>(kp, valid, px, py, lp, h, lds4);
     if (!valid) return;
     const long long Pc = kp.Pc;
     const long long ci = static_cast<long long>(py) * kp.Wh + (px >> 1);
-    float4 ph;
-    if (h < 8) {
-        const int pos = pick_neighbour(kp, h, px, py);
-        kp.nbpos[h * Pc + ci] = pos;
-        if (pos < 0) return;
-        ph = plane_at(kp, pos);
-    } else {
-        ph = kp.plane_cs[colour][ci];
-    }
+    const int pos = pick_neighbour(kp, h, px, py);
+    kp.nbpos[h * Pc + ci] = pos;
+    if (pos < 0) return;
+    const float4 ph = plane_at(kp, pos);
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
-    for_all_views<MODEL, VB, 1, false>(kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
+    for_all_views<MODEL, VB, 3, false>(kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
 }
 
 // Joint view selection, aggregation, acceptance and refinement candidates (ACMMP.cu:1146-1311,
 // 797-874).  `iter` selects the view-selection threshold 0.8 exp(-iter^2 / 90) (:1163).
-template <int MODEL>
+template <int MODEL, int VB, bool GEOM>
 __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colour, const int iter) {
     const long long q = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
     int px = 0, py = 0;
@@ -1059,7 +1119,8 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
     };
 
     // ---- joint view selection :1146-1208
-    float vsp[kMaxViews];
+    constexpr int VMAX = VB < 8 ? VB : kMaxViews;            // pick_vb: V <= VB when VB < 8
+    float vsp[VMAX];
     for (int j = 0; j < V; ++j) vsp[j] = 0.0f;
     {
         const int nbx[4] = {px, px, px - 1, px + 1};
@@ -1074,7 +1135,7 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
     }
     const float cost_threshold = static_cast<float>(0.8 * static_cast<double>(
         det_exp(static_cast<float>(iter * iter) / (-90.0f))));
-    float probs[kMaxViews];
+    float probs[VMAX];
     for (int i = 0; i < V; i++) {
         float count = 0.0f;
         int count_false = 0;
@@ -1120,11 +1181,11 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
     for (int i = 0; i < 8; ++i) {
         float fc = 0.0f;
         float4 nb = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (kp.geom && flag[i]) nb = plane_at(kp, pos[i]);
+        if (GEOM && flag[i]) nb = plane_at(kp, pos[i]);
         for (int j = 0; j < V; ++j) {
             const float w = vw_get(vwp, j);
             if (w > 0) {
-                if (kp.geom) {
+                if (GEOM) {
                     if (flag[i]) fc = fmaf(w, fmaf(0.2f, geom_cost<MODEL>(kp, j + 1, nb, px, py, dc), cost_arr(i, j)), fc);
                     else fc = fmaf(w, cost_arr(i, j) + 0.1f * 3.0f, fc);
                 } else {
@@ -1143,12 +1204,28 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
 
     // ---- current hypothesis :1232-1245 (zero-weight views add +0: skipped)
     float4 cur_plane = kp.plane_cs[colour][ci];
+    // the current plane's NCC cost vector is cached from when it was evaluated (k_init, or as the
+    // neighbour hypothesis / refinement candidate that won the last sweep).  Views the cache lacks
+    // (a candidate whose wave skipped a view) are evaluated here; that is rare and only for them.
+    float* cvec = kp.cvec[colour] + ci;
+    uint32_t miss = 0u;
+    for (int v = 0; v < V; ++v)
+        if (vw_get(vwp, v) > 0.0f && cvec[v * Pc] != cvec[v * Pc]) miss |= 1u << v;
+#ifdef ACMMP_EXP_NOFILL
+    miss = 0u;                                              // A/B experiment only (wrong results)
+#endif
+    if (miss) {
+        const Patch pt = make_patch<MODEL>(kp, px, py);
+        for_all_views<MODEL, 1, 0, true>(kp, px, py, pt, cur_plane, wave_or(miss, V), [&](int v, float c) {
+            if ((miss >> v) & 1u) cvec[v * Pc] = c;
+        });
+    }
     float cost_now = 0.0f;
     for (int v = 0; v < V; ++v) {
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
-            const float c = kp.hyp_cost[(static_cast<long long>(8) * V + v) * Pc + ci];
-            if (kp.geom) cost_now = fmaf(w, fmaf(0.2f, geom_cost<MODEL>(kp, v + 1, cur_plane, px, py, dc), c), cost_now);
+            const float c = cvec[v * Pc];
+            if (GEOM) cost_now = fmaf(w, fmaf(0.2f, geom_cost<MODEL>(kp, v + 1, cur_plane, px, py, dc), c), cost_now);
             else cost_now = fmaf(w, c, cost_now);
         }
     }
@@ -1158,6 +1235,7 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
     float depth_now = depth_from_plane(cur_plane, dc);
     float restricted_cost = 0.0f;
     const bool use_prior = kp.planar && kp.mask[center] > 0;
+    int src_cur = 8;                                        // hypothesis ids, see PixState::src
 
     auto sel_pos = [&](int i) -> int {
         int r = pos[0];
@@ -1215,6 +1293,7 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
                     cur_cost = sel_f(final_costs, max_idx);
                     restricted_cost = rmax;
                     cur_sel = temp_sel;
+                    src_cur = max_idx;
                 }
             }
         } else {
@@ -1227,12 +1306,14 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
                     depth_now = db;
                     cur_plane = nb;
                     cur_cost = fmin;
+                    src_cur = min_idx;
                 }
             }
         }
     }
 
     float4 plane_now = cur_plane;                           // fix A (:1301)
+    int src_now = src_cur;
     if (!kp.planar) {                                       // :1302-1311
         const int mpos = sel_pos(min_idx);
         if (mpos >= 0) {
@@ -1244,6 +1325,7 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
                 plane_now = nb;
                 cost_now = fmin;
                 cur_sel = temp_sel;
+                src_now = min_idx;
             }
         }
     }
@@ -1298,13 +1380,13 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
     st.cur_sel = cur_sel;
     st.flags = flags;
     st.weight_norm = weight_norm;
-    st.pad = 0u;
+    st.src = static_cast<uint32_t>(src_now) | (static_cast<uint32_t>(src_cur) << 8);
     kp.pst[ci] = st;
     kp.rng_cs[colour][ci] = rs.n;
 }
 
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
-template <int MODEL, int VB>
+template <int MODEL, int VB, bool GEOM>
 __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int colour) {
     extern __shared__ float2 lds2[];
     const int t = threadIdx.x;
@@ -1332,10 +1414,15 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
     uint32_t mask = 0u;
     for (int v = 0; v < kp.V; ++v) if (vw_get(vwp, v) > 0.0f) mask |= 1u << v;
     float temp_cost = 0.0f;
-    for_all_views<MODEL, VB, 2, true>(kp, px, py, pt, tp, wave_or(mask, kp.V), [&](int v, float c) {
+    const uint32_t umask = wave_or(mask, kp.V);
+    float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
+    for (int v = 0; v < kp.V; ++v)
+        if (!((umask >> v) & 1u)) vcost[v * Pc] = __builtin_nanf("");
+    for_all_views<MODEL, VB, 2, true>(kp, px, py, pt, tp, umask, [&](int v, float c) {
+        vcost[v * Pc] = c;
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
-            if (kp.geom) temp_cost = fmaf(w, fmaf(0.1f, geom_cost<MODEL>(kp, v + 1, tp, px, py, dc), c), temp_cost);
+            if (GEOM) temp_cost = fmaf(w, fmaf(0.1f, geom_cost<MODEL>(kp, v + 1, tp, px, py, dc), c), temp_cost);
             else temp_cost = fmaf(w, c, temp_cost);
         }
     });
@@ -1356,6 +1443,8 @@ __global__ __launch_bounds__(256) void k_finish(const KParams kp, const int colo
     float4 plane_now = st.plane_now;
     float cost_now = st.cost_now;
     float restricted_cost = st.restricted_cost;
+    int src_now = static_cast<int>(st.src & 255u);
+    const int src_cur = static_cast<int>((st.src >> 8) & 255u);
     if (st.flags & 2u) {
         const bool use_prior = (st.flags & 1u) != 0u;
         const float gamma = 0.5f;
@@ -1381,20 +1470,31 @@ __global__ __launch_bounds__(256) void k_finish(const KParams kp, const int colo
                 const float ad = det_acos(ac);
                 const float pr = fmaf(det_exp((-ddiff) * ddiff / two_dss), det_exp((-ad) * ad / two_ass), gamma);
                 const float rtc = det_exp((-temp_cost) * temp_cost / beta) * pr;
-                if (rtc > restricted_cost) { plane_now = tp; cost_now = temp_cost; restricted_cost = rtc; }
+                if (rtc > restricted_cost) {
+                    plane_now = tp; cost_now = temp_cost; restricted_cost = rtc; src_now = 9 + i;
+                }
             } else if (temp_cost < cost_now) {
                 plane_now = tp;
                 cost_now = temp_cost;
+                src_now = 9 + i;
             }
         }
     }
     float4 cur_plane = st.cur_plane;
     float cur_cost = st.cur_cost;
+    int src = src_cur;
     if (kp.hier) {
-        if (cost_now < kp.pre_rm[center] - 0.1f) { cur_cost = cost_now; cur_plane = plane_now; }
+        if (cost_now < kp.pre_rm[center] - 0.1f) { cur_cost = cost_now; cur_plane = plane_now; src = src_now; }
     } else {
         cur_cost = cost_now;
         cur_plane = plane_now;
+        src = src_now;
+    }
+    if (src != 8) {                                          // keep the cost-vector cache in step
+        const float* from = src < 8 ? kp.hyp_cost + static_cast<long long>(src) * kp.V * Pc + ci
+                                    : kp.cand_vcost + static_cast<long long>(src - 9) * kp.V * Pc + ci;
+        float* to = kp.cvec[colour] + ci;
+        for (int v = 0; v < kp.V; ++v) to[v * Pc] = from[v * Pc];
     }
     out.plane[ci] = cur_plane;
     out.cost[ci] = cur_cost;
@@ -1570,23 +1670,31 @@ static inline int pick_vb(int V) { return V <= 1 ? 1 : (V <= 2 ? 2 : (V <= 4 ? 4
 
 hipError_t launch_init(const KParams& kp, hipStream_t s) {
     dim3 blk(16, 16), grd(cdiv(kp.W, 16), cdiv(kp.H, 16));
-    ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC><<<grd, blk, 0, s>>>(kp)));
+    // branch order of ACMMP.cu:686-793
+    const int br = (!kp.geom && !kp.hier) ? kInitRandom : kp.planar ? kInitPlanar : kp.upsample ? kInitUpsample
+                                                                                                 : kInitReuse;
+    if (br == kInitRandom) ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC, kInitRandom><<<grd, blk, 0, s>>>(kp)));
+    else if (br == kInitPlanar) ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC, kInitPlanar><<<grd, blk, 0, s>>>(kp)));
+    else if (br == kInitUpsample)
+        ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC, kInitUpsample><<<grd, blk, 0, s>>>(kp)));
+    else ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC, kInitReuse><<<grd, blk, 0, s>>>(kp)));
     return hipGetLastError();
 }
 
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s, hipEvent_t* ev) {
     const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
-    const size_t lds_nb = (sizeof(float4) + sizeof(float)) * kNbPix * kp.S;
+    const size_t lds_nb = nb_lds_bytes(kp.model, kp.S, kp.nside);
     const size_t lds_ref = sizeof(float2) * kRefPix * kp.S;
     hipError_t e = hipSuccess;
 #define ACMMP_MARK(i) if (ev && (e = hipEventRecord(ev[i], s)) != hipSuccess) return e
     ACMMP_MARK(0);
     ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC><<<cdiv(npix, kNbPix), 256, lds_nb, s>>>(kp, colour)));
     ACMMP_MARK(1);
-    if (kp.model == kSphere) k_select<kSphere><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter);
-    else k_select<kPinhole><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter);
+    if (kp.geom) ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, true><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
+    else ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, false><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
     ACMMP_MARK(2);
-    ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC><<<cdiv(npix, kRefPix), 256, lds_ref, s>>>(kp, colour)));
+    if (kp.geom) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, true><<<cdiv(npix, kRefPix), 256, lds_ref, s>>>(kp, colour)));
+    else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, false><<<cdiv(npix, kRefPix), 256, lds_ref, s>>>(kp, colour)));
     ACMMP_MARK(3);
     if (kp.model == kSphere) k_finish<kSphere><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, out);
     else k_finish<kPinhole><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, out);
