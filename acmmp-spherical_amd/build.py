@@ -19,7 +19,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["kernels.hip", "capi.cpp", "comm.cpp", "planar_prior.cpp"]
 HIP_CPP = {"capi.cpp", "comm.cpp"}              # host C++ that includes HIP headers
 HEADERS = ["engine.h", "detmath.h"]
-COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}",
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize", f"--offload-arch={ARCH}",
           f"-I{INCLUDE}", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
 
 
@@ -27,7 +27,8 @@ def _newest(paths):
     return max(os.path.getmtime(p) for p in paths)
 
 
-def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines=(), objdir: str | None = None) -> str:
+def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines=(), objdir: str | None = None,
+          flags=()) -> str:
     """Compile csrc/ into `lib`.  `defines` (e.g. ["ACMMP_EXPERIMENT=1"]) + a separate `objdir` give an
     experiment variant next to the product build (select it at run time with ACMMP_LIB=<path>)."""
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(INCLUDE, "acmmp.h")]
@@ -42,7 +43,7 @@ def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines=(),
         hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "acmmp.h")]
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < _newest([srcp] + hdrs):
             lang = ["-x", "hip"] if src in HIP_CPP else []
-            cmd = [HIPCC, *COMMON, *[f"-D{d}" for d in defines], *lang, "-c", srcp, "-o", obj]
+            cmd = [HIPCC, *COMMON, *flags, *[f"-D{d}" for d in defines], *lang, "-c", srcp, "-o", obj]
             if verbose:
                 print("[acmmp build]", " ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)

@@ -132,6 +132,21 @@ __device__ __forceinline__ float sqrt_proj(float x) {
     return fmaf(-sup, s, x) > 0.0f ? sup : r;
 }
 
+// det_asin with its large-argument square root through sqrt_proj: there z = (1 - |x|) / 2 is 0, NaN,
+// negative (|x| > 1 by rounding) or >= 2^-25 (1 - |x| is exact and at least 2^-24), where sqrt_proj
+// equals sqrtf bit for bit.
+__device__ __forceinline__ float asin_proj(float x) {
+    const float a = fabsf(x);
+    float r;
+    if (a <= 0.5f) {
+        r = det_asin_core(a, a * a);
+    } else {
+        const float z = (1.0f - a) * 0.5f;
+        r = fmaf(-2.0f, det_asin_core(sqrt_proj(z), z), kPio2Hi) + kPio2Lo;
+    }
+    return copysignf(r, x);
+}
+
 // ProjectonCamera_cu, ACMMP.cu:602-644 (Cam: DevCam in any address space)
 template <int MODEL, typename Cam>
 __device__ __forceinline__ void project(Cam& c, float3 P, float& ox, float& oy, float& depth) {
@@ -141,7 +156,7 @@ __device__ __forceinline__ void project(Cam& c, float3 P, float& ox, float& oy, 
     if (MODEL == kSphere) {
         const float d = sqrt_proj(dot3(tx, ty, tz, tx, ty, tz));
         depth = d;
-        const float neg_lat = det_asin(ty / d);
+        const float neg_lat = asin_proj(ty / d);
         const float lon = det_atan2(tx, tz);
         ox = fmaf(lon * kInv2Pi, c.Wf, c.cx);
         oy = fmaf(neg_lat * kInvPi, c.Hf, c.cy);
@@ -337,51 +352,6 @@ __device__ __forceinline__ Patch make_patch(const KParams& kp, int px, int py) {
     return pt;
 }
 
-// Projection parameters of one source view, loaded once per chunk (wave-uniform -> SGPRs).
-struct ProjCam {
-    float R[9], t[3], K[6];
-    float Wf, Hf, invW, cx, cy;
-    int W, H, pitch;
-    const float* img;
-};
-
-__device__ __forceinline__ ProjCam load_projcam(const KParams& kp, int view) {
-    const DevCam& c = kp.cams[uniform_int(view)];
-    ProjCam p;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) p.R[k] = c.R[k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) p.t[k] = c.t[k];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) p.K[k] = c.K[k];
-    p.Wf = c.Wf; p.Hf = c.Hf; p.invW = c.invW; p.cx = c.cx; p.cy = c.cy;
-    p.W = c.W; p.H = c.H; p.pitch = c.img_pitch;
-    p.img = kp.img + c.img_off;
-    return p;
-}
-
-// ProjectonCamera_cu (ACMMP.cu:602-644) on a ProjCam; identical arithmetic to project<MODEL>.
-template <int MODEL>
-__device__ __forceinline__ void project_pc(const ProjCam& c, float3 P, float& ox, float& oy) {
-    const float tx = dot3(c.R[0], c.R[1], c.R[2], P.x, P.y, P.z) + c.t[0];
-    const float ty = dot3(c.R[3], c.R[4], c.R[5], P.x, P.y, P.z) + c.t[1];
-    const float tz = dot3(c.R[6], c.R[7], c.R[8], P.x, P.y, P.z) + c.t[2];
-    if (MODEL == kSphere) {
-        const float d = sqrtf(dot3(tx, ty, tz, tx, ty, tz));
-        const float neg_lat = det_asin(ty / d);
-        const float lon = det_atan2(tx, tz);
-        ox = fmaf(lon * kInv2Pi, c.Wf, c.cx);
-        oy = fmaf(neg_lat * kInvPi, c.Hf, c.cy);
-        if (d < 1e-6f) { ox = c.cx; oy = c.cy; }
-    } else {
-        const float inv = 1.0f / tz;
-        ox = dot3(c.K[0], c.K[1], c.K[2], tx, ty, tz) * inv;
-        oy = dot3(c.K[3], c.K[4], c.K[5], tx, ty, tz) * inv;
-    }
-}
-
-// ComputeBilateralNCC (ACMMP.cu:405-516) of plane `ph` at pixel (px, py) against the
-// source views vlist[0..nv) (wave-uniform camera indices 1..N-1), sample-outer.
 // STAGED: 0 = samples recomputed here, 1 = (ray, w) + texel staged in LDS, 2 = (w, texel) staged
 // and the ray re-read from the ray tables (less LDS per pixel, more blocks per CU), 3 = the
 // k_eval_nb layout of coop_patch_nb.
