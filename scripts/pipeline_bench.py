@@ -1,0 +1,56 @@
+"""End-to-end timing of the multi-pass pipeline (main.cpp's schedule) on a synthetic SPHERE scene.
+
+python scripts/pipeline_bench.py [--views 6] [--width 2000] [--height 1000]
+Prints one JSON line: per-pass wall times, total, and depth accuracy of the final maps.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "acmmp-spherical_amd"))
+
+import numpy as np  # noqa: E402
+
+from acmmp import io, pipeline, scene  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--views", type=int, default=6)
+    ap.add_argument("--width", type=int, default=2000)
+    ap.add_argument("--height", type=int, default=1000)
+    ap.add_argument("--seed", type=int, default=5)
+    a = ap.parse_args()
+    sc = scene.sphere_scene(a.width, a.height, n_src=a.views - 1, seed=a.seed)
+    images = {i: np.asarray(sc.images[i], np.float32) for i in range(a.views)}
+    cams = {i: np.array(sc.cameras[i], copy=True) for i in range(a.views)}
+    problems = []
+    for i in range(a.views):
+        p = io.Problem(i)
+        p.src_image_ids = [j for j in range(a.views) if j != i]
+        problems.append(p)
+    ds = pipeline.Dataset(images, cams, problems)
+    times = []
+    last = [time.perf_counter()]
+
+    def log(msg):
+        now = time.perf_counter()
+        times.append((msg, now - last[0]))
+        last[0] = now
+        print(msg, flush=True)
+
+    t0 = time.perf_counter()
+    pipe = pipeline.Pipeline(ds, order="reference", log=log).run()
+    total = time.perf_counter() - t0
+    d0 = pipe.store.get("depths_geom", 0)
+    acc = scene.depth_accuracy(d0, sc.gt_depth) if d0.shape == sc.gt_depth.shape else None
+    print(json.dumps({"views": a.views, "size": [a.width, a.height], "passes": [p.name for p in pipe.passes],
+                      "total_s": round(total, 3), "s_per_view_pass": round(total / (a.views * len(pipe.passes)), 4),
+                      "ref_view_frac_within_1pct_gt": acc}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
