@@ -68,6 +68,8 @@ struct acmmp_ctx {
     float timing[3] = {0.f, 0.f, 0.f};
     std::vector<hipEvent_t> kev;               // 5 per half-sweep (per-kernel timing)
     float ktiming[4] = {0.f, 0.f, 0.f, 0.f};
+    unsigned long long* d_work = nullptr;       // [256] k_eval_nb work counters
+    unsigned long long work_busy = 0, work_total = 0;
     int klaunch[4] = {0, 0, 0, 0};
     std::string err;
 };
@@ -163,7 +165,7 @@ void acmmp_destroy(acmmp_ctx* c) {
     dfree(c->d_cams); dfree(c->d_img); dfree(c->d_dep); dfree(c->d_dirs);
     dfree(c->d_sph_row); dfree(c->d_sph_col); dfree(c->d_spatial);
     dfree(c->d_planes_rm); dfree(c->d_costs_rm); dfree(c->d_pre); dfree(c->d_sel_rm);
-    dfree(c->d_scaled); dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_scratch);
+    dfree(c->d_scaled); dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_scratch); dfree(c->d_work);
     for (int k = 0; k < 2; ++k) {
         for (int b = 0; b < 2; ++b) { dfree(c->d_plane_cs[k][b]); dfree(c->d_cost_cs[k][b]); }
         dfree(c->d_sel_cs[k]); dfree(c->d_rng_cs[k]);
@@ -360,6 +362,16 @@ acmmp_status acmmp_set_planar_prior(acmmp_ctx* c, const float* prior, const uint
     return ACMMP_OK;
 }
 
+// pixels of one colour inside the checkerboard grid (the half-sweep's work items)
+static unsigned long long colour_pixels(const acmmp_ctx* c, const KParams& kp, int colour) {
+    unsigned long long n = 0;
+    for (int y = 0; y < kp.rows; ++y) {
+        const int first = (y + colour) & 1;                  // black = (x + y) even
+        n += first < c->W ? static_cast<unsigned long long>((c->W - first + 1) / 2) : 0ull;
+    }
+    return n;
+}
+
 static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     const acmmp_params& p = c->params;
     if (!c->has_params) return fail(c, ACMMP_ERR_STATE, "set_params first");
@@ -450,6 +462,8 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.cvec[0] = reinterpret_cast<float*>(c->d_scratch + off[6]);
     kp.cvec[1] = reinterpret_cast<float*>(c->d_scratch + off[7]);
     kp.cand_vcost = reinterpret_cast<float*>(c->d_scratch + off[8]);
+    if (!c->d_work) HIP_TRY(c, dalloc(c->d_work, 256));
+    kp.work = c->d_work;
     return ACMMP_OK;
 }
 
@@ -462,6 +476,7 @@ acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx* c, uint64_t seed, int n_half_swe
     if (n_half_sweeps < 0) n_half_sweeps = 2 * c->params.max_iterations;
     const size_t Pc = static_cast<size_t>(kp.Pc);
     hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long) * 256, s));
     HIP_TRY(c, hipEventRecord(c->ev[0], s));
     HIP_TRY(c, launch_init(kp, s));
     // rows outside the reference's checkerboard grid are never rewritten: keep both buffers equal
@@ -498,6 +513,14 @@ acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx* c, uint64_t seed, int n_half_swe
         }
     }
     for (int i = 0; i < 3; ++i) HIP_TRY(c, hipEventElapsedTime(&c->timing[i], c->ev[i], c->ev[i + 1]));
+    {
+        unsigned long long w[256];
+        HIP_TRY(c, hipMemcpy(w, c->d_work, sizeof w, hipMemcpyDeviceToHost));
+        c->work_busy = 0;
+        for (int k = 0; k < 256; ++k) c->work_busy += w[k];
+        c->work_total = 0;
+        for (int sw = 0; sw < n_half_sweeps; ++sw) c->work_total += colour_pixels(c, kp, sw & 1);
+    }
     for (int k = 0; k < 4; ++k) { c->ktiming[k] = 0.f; c->klaunch[k] = n_half_sweeps; }
     for (int sw = 0; sw < n_half_sweeps; ++sw)
         for (int k = 0; k < 4; ++k) {
@@ -547,6 +570,13 @@ acmmp_status acmmp_synchronize(acmmp_ctx* c) {
 acmmp_status acmmp_last_timing(const acmmp_ctx* c, float ms[3]) {
     if (!c || !ms) return ACMMP_ERR_INVALID_ARGUMENT;
     for (int i = 0; i < 3; ++i) ms[i] = c->timing[i];
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_last_work(const acmmp_ctx* c, unsigned long long* evaluated, unsigned long long* total) {
+    if (!c || !evaluated || !total) return ACMMP_ERR_INVALID_ARGUMENT;
+    *evaluated = c->work_busy;
+    *total = c->work_total;
     return ACMMP_OK;
 }
 

@@ -95,6 +95,7 @@ struct KParams {
     float* cand_dep;                // [5][Pc] their depths (prior term, ACMMP.cu:912)
     float* cand_cost;               // [5][Pc] their aggregated costs
     PixState* pst;                  // [Pc]
+    unsigned long long* work;       // [256] k_eval_nb pixels with NCC work (SPHERE patch sum >= 1e-6), per block % 256
     long long Pc;                   // H * Wh
 };
 

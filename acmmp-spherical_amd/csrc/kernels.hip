@@ -358,6 +358,14 @@ __device__ __forceinline__ Patch make_patch(const KParams& kp, int px, int py) {
 template <int MODEL, int VB, int STAGED, bool PIPE>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv, float (&cost)[VB]) {
+    // SPHERE: the weight sum of every view is the pixel's patch sum (hypothesis- and view-independent);
+    // below 1e-6 each cost is 2.0 (ACMMP.cu:501-503) whatever the samples, so they are not evaluated.
+    // (The SPHERE sigma-in-radians band of SURVEY.md §0.5 puts ~40% of a 2000x1500 view here.)
+    if (MODEL == kSphere && pt.sbw < 1e-6f) {
+#pragma unroll
+        for (int v = 0; v < VB; ++v) cost[v] = 2.0f;
+        return;
+    }
     const DevCam& rc = kp.cams[0];
     float sbw[VB], sref[VB], srr[VB], ssrc[VB], sss[VB], srs[VB];
     bool cval[VB];
@@ -963,6 +971,9 @@ __device__ __forceinline__ Patch coop_patch(const KParams& kp, bool valid, int p
 // per sample and ray.y = -sin(lat) once per patch row (it depends on the row only); PINHOLE stores
 // (ray, w) per sample and the texels after them.  32 pixels x 36 samples = 19.2 KB per block for
 // SPHERE (8 blocks per CU).
+#ifndef ACMMP_NB_PIPE
+#define ACMMP_NB_PIPE false                 // experiment switch: all views' texels in flight in k_eval_nb
+#endif
 constexpr int kNbLanes = 8;                 // the 8 neighbour directions (the current plane's costs are cached)
 constexpr int kNbPix = 32;                  // pixels per 256-lane block
 
@@ -1045,6 +1056,9 @@ __global__ __launch_bounds__(256, 8) void k_eval_nb(const KParams kp, const int 
     int px = 0, py = 0;
     const bool valid = colour_pixel(kp, colour, q, px, py);
     const Patch pt = coop_patch_nb<MODEL>(kp, valid, px, py, lp, h, lds4);
+    // work accounting for the roofline: pixels whose NCCs are evaluated (not short-circuited)
+    const int busy = __syncthreads_count(valid && h == 0 && !(MODEL == kSphere && pt.sbw < 1e-6f));
+    if (t == 0 && busy) atomicAdd(kp.work + (blockIdx.x & 255u), static_cast<unsigned long long>(busy));
     if (!valid) return;
     const long long Pc = kp.Pc;
     const long long ci = static_cast<long long>(py) * kp.Wh + (px >> 1);
@@ -1054,7 +1068,7 @@ __global__ __launch_bounds__(256, 8) void k_eval_nb(const KParams kp, const int 
     const float4 ph = plane_at(kp, pos);
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
-    for_all_views<MODEL, VB, 3, false>(kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
+    for_all_views<MODEL, VB, 3, ACMMP_NB_PIPE>(kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
 }
 
 // Joint view selection, aggregation, acceptance and refinement candidates (ACMMP.cu:1146-1311,

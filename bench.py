@@ -70,6 +70,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 -> min(16, os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variant", action="store_true", help="skip the non-degenerate 2000x1000 side measurement")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_propagate.json"),
                     help="rocprofv3 PMC summary giving HBM bytes per propagation launch")
     return ap.parse_args()
@@ -79,6 +80,34 @@ def make_scene(args, rank: int):
     if args.model == "sphere":
         return scene.sphere_scene(args.width, args.height, n_src=args.n_src, seed=args.seed + 7919 * rank)
     return scene.pinhole_scene(args.width, args.height, n_src=args.n_src, seed=args.seed + 7919 * rank)
+
+
+def nondegenerate_variant(args, ctx, width=2000, height=1000, steps=3):
+    """the metric's 2000x1500 SPHERE view puts ~40% of its pixels in the reference's
+    sigma-in-radians band (every cost 2.0, short-circuited here); report the 2:1 equirectangular
+    2000x1000 view beside it, where every pixel does NCC work.  Reported, never `value`."""
+    sc = scene.sphere_scene(width, height, n_src=args.n_src, seed=args.seed + 1)
+    c0 = sc.cameras[0]
+    p = types.default_params(num_images=args.n_src + 1, max_iterations=args.iters,
+                             depth_min=float(c0["depth_min"]) * 0.6, depth_max=float(c0["depth_max"]) * 1.2)
+    ctx.set_params(p)
+    ctx.upload_views(sc.images, sc.cameras)
+    ctx.run_patchmatch(args.seed + 999)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    nb_ms = 0.0
+    for k in range(steps):
+        ctx.run_patchmatch(args.seed + k)
+        nb_ms += ctx.last_kernel_timing()["k_eval_nb"][0]
+    ctx.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    ev, tot = ctx.last_work()
+    planes, _ = ctx.download()
+    return {"config": f"RunPatchMatch {width}x{height} sphere, 1 ref + {args.n_src} src, {args.iters} iterations",
+            "value": round(width * height * args.iters / dt / 1e6, 3), "unit": "Mpixel-iterations/s",
+            "ms_per_depth_map": round(dt * 1e3, 3), "k_eval_nb_ms": round(nb_ms / steps / (2 * args.iters), 4),
+            "short_circuited_pixel_frac": round(1.0 - ev / max(tot, 1), 4),
+            "frac_within_1pct_gt": round(scene.depth_accuracy(planes[..., 3], sc.gt_depth), 4)}
 
 
 def cpu_baseline(args, sc, params, gpu_rate_check=None):
@@ -157,6 +186,7 @@ def main():
     t0 = time.perf_counter()
     stage = np.zeros(3)
     kern = {k: [0.0, 0] for k in capi.Context.KERNELS}
+    work = [0, 0]                        # k_eval_nb pixels evaluated / processed (SPHERE short-circuit)
     for k in range(args.steps):
         ctx.run_patchmatch(args.seed + k)
         tm = ctx.last_timing()
@@ -164,6 +194,9 @@ def main():
         for name, (ms, n) in ctx.last_kernel_timing().items():
             kern[name][0] += ms
             kern[name][1] += n
+        ev, tot = ctx.last_work()
+        work[0] += ev
+        work[1] += tot
     ctx.synchronize()
     barrier()
     ctx.synchronize()
@@ -191,7 +224,9 @@ def main():
     nb_ms, nb_n = kern["k_eval_nb"]
     launch_ms = nb_ms / max(nb_n, 1)
     rows = min(args.height, 32 * (((args.height // 2) + 15) // 16))
-    pix_per_launch = rows * args.width / 2.0
+    # algorithmic work = pixels whose NCCs are evaluated; SPHERE pixels whose patch weight sum is
+    # < 1e-6 have every cost = 2.0 without evaluating a sample (ACMMP.cu:501-503) and are not counted
+    pix_per_launch = work[0] / max(nb_n, 1)
     flop_launch = eval_nb_flop_per_pixel(args.model, args.n_src) * pix_per_launch
     achieved = flop_launch / (launch_ms * 1e-3) / 1e12
     traffic = None
@@ -219,17 +254,22 @@ def main():
         "launch_ms": round(launch_ms, 4),
         "launches": nb_n,
         "flop_per_launch": flop_launch,
+        "evaluated_pixels_per_launch": round(pix_per_launch),
+        "short_circuited_pixel_frac": round(1.0 - work[0] / max(work[1], 1), 4),
         "hbm": hbm,
         "half_sweep_kernels_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items()},
-        "half_sweep_reference_flop_tflops": round(algorithmic_flop_per_pixel(args.model, args.n_src) / 2.0 *
-                                            rows * args.width / (sum(v[0] for v in kern.values()) /
-                                                                 max(nb_n, 1) * 1e-3) / 1e12, 3),
+        "half_sweep_reference_flop_tflops": round(algorithmic_flop_per_pixel(args.model, args.n_src) *
+                                                  pix_per_launch / (sum(v[0] for v in kern.values()) /
+                                                                    max(nb_n, 1) * 1e-3) / 1e12, 3),
         "note": "FP32 vector peak (equal to the f32 MFMA dense peak); the path has no GEMM-shaped work",
     }
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, sc, params)
+    variant = None
+    if rank == 0 and world == 1 and args.model == "sphere" and not args.no_variant:
+        variant = nondegenerate_variant(args, ctx)
 
     if rank == 0:
         line = {
@@ -259,6 +299,7 @@ def main():
             "quality": {"frac_within_1pct_gt": round(acc, 4), "nan_cost_frac": round(nan_frac, 4)},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "nondegenerate_variant": variant,
         }
         print(json.dumps(line), flush=True)
     ctx.close()

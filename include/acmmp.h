@@ -160,6 +160,11 @@ acmmp_status acmmp_last_timing(const acmmp_ctx *ctx, float ms[3]);
  * (the four kernels one CheckerboardPropagation half-sweep is split into). */
 acmmp_status acmmp_last_kernel_timing(const acmmp_ctx *ctx, float ms[4], int launches[4]);
 
+/* Work accounting of the last run's k_eval_nb launches: pixels whose NCCs were evaluated, and all
+ * pixels processed.  SPHERE pixels whose patch weight sum is below 1e-6 have every cost = 2.0
+ * (ACMMP.cu:501-503) and are short-circuited; the roofline counts only evaluated pixels. */
+acmmp_status acmmp_last_work(const acmmp_ctx *ctx, unsigned long long *evaluated, unsigned long long *total);
+
 /* ---- device buffers and the multi-GPU communicator (no reference counterpart:
  * the reference is single-GPU and exchanges depth maps through dmb files) ------------------- */
 
