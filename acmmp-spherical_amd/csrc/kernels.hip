@@ -977,21 +977,21 @@ __device__ __forceinline__ Patch coop_patch(const KParams& kp, bool valid, int p
 constexpr int kNbLanes = 8;                 // the 8 neighbour directions (the current plane's costs are cached)
 constexpr int kNbPix = 32;                  // pixels per 256-lane block
 
-static inline size_t nb_lds_bytes(int model, int S, int nside) {
-    return model == kSphere ? (sizeof(float4) * S + sizeof(float) * nside) * kNbPix
-                            : (sizeof(float4) + sizeof(float)) * S * kNbPix;
+static inline size_t nb_lds_bytes(int model, int S, int nside, int npix = kNbPix) {
+    return model == kSphere ? (sizeof(float4) * S + sizeof(float) * nside) * npix
+                            : (sizeof(float4) + sizeof(float)) * S * npix;
 }
 
-template <int MODEL>
+template <int MODEL, int NPIX = kNbPix, int NLANES = kNbLanes>
 __device__ __forceinline__ Patch coop_patch_nb(const KParams& kp, bool valid, int px, int py, int lp, int h,
                                                float4* lds) {
     float4* rw = lds + lp * kp.S;
-    float* tail = reinterpret_cast<float*>(lds + kNbPix * kp.S);
+    float* tail = reinterpret_cast<float*>(lds + NPIX * kp.S);
     float* rr = tail + lp * (MODEL == kSphere ? kp.nside : kp.S);
     if (valid) {
         const DevCam& rc = kp.cams[0];
         const float center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
-        for (int s = h; s < kp.S; s += kNbLanes) {
+        for (int s = h; s < kp.S; s += NLANES) {
             const int i = -kp.R + (s / kp.nside) * kp.inc, j = -kp.R + (s % kp.nside) * kp.inc;
             float r;
             const float4 q = patch_sample<MODEL>(kp, px, py, s, i, j, center, r);
@@ -1372,7 +1372,7 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
 template <int MODEL, int VB, bool GEOM>
 __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int colour) {
-    extern __shared__ float2 lds2[];
+    extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
     const long long q = static_cast<long long>(blockIdx.x) * kRefPix + lp;
@@ -1388,7 +1388,7 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
         vw = st.vw;
         weight_norm = st.weight_norm;
     }
-    const Patch pt = coop_patch_lite<MODEL>(kp, valid, px, py, lp, h, kRefLanes, lds2);
+    const Patch pt = coop_patch_nb<MODEL, kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
     if (!valid) return;
     const float4 dc = ray_at<MODEL>(kp, px, py);
     const float4 tp = kp.cand[h * Pc + ci];
@@ -1402,7 +1402,7 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
     float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
     for (int v = 0; v < kp.V; ++v)
         if (!((umask >> v) & 1u)) vcost[v * Pc] = __builtin_nanf("");
-    for_all_views<MODEL, VB, 2, true>(kp, px, py, pt, tp, umask, [&](int v, float c) {
+    for_all_views<MODEL, VB, 3, true>(kp, px, py, pt, tp, umask, [&](int v, float c) {
         vcost[v * Pc] = c;
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
@@ -1668,7 +1668,7 @@ hipError_t launch_init(const KParams& kp, hipStream_t s) {
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s, hipEvent_t* ev) {
     const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
     const size_t lds_nb = nb_lds_bytes(kp.model, kp.S, kp.nside);
-    const size_t lds_ref = sizeof(float2) * kRefPix * kp.S;
+    const size_t lds_ref = nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
     hipError_t e = hipSuccess;
 #define ACMMP_MARK(i) if (ev && (e = hipEventRecord(ev[i], s)) != hipSuccess) return e
     ACMMP_MARK(0);
