@@ -1104,8 +1104,11 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
 
     // ---- joint view selection :1146-1208
     constexpr int VMAX = VB < 8 ? VB : kMaxViews;            // pick_vb: V <= VB when VB < 8
+    // loops over views run to the compile-time VMAX with a guard, so the per-view arrays stay in
+    // registers (statically indexed) instead of scratch
     float vsp[VMAX];
-    for (int j = 0; j < V; ++j) vsp[j] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < VMAX; ++j) vsp[j] = 0.0f;
     {
         const int nbx[4] = {px, px, px - 1, px + 1};
         const int nby[4] = {py - 1, py + 1, py, py};
@@ -1113,14 +1116,19 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
         for (int i = 0; i < 4; ++i) {
             if (flag[2 * i]) {
                 const uint32_t sv = kp.sel_cs[(nbx[i] + nby[i]) & 1][cs_index(kp, nbx[i], nby[i])];
-                for (int j = 0; j < V; ++j) vsp[j] += ((sv >> j) & 1u) ? 0.9f : 0.1f;
+#pragma unroll
+                for (int j = 0; j < VMAX; ++j)
+                    if (j < V) vsp[j] += ((sv >> j) & 1u) ? 0.9f : 0.1f;
             }
         }
     }
     const float cost_threshold = static_cast<float>(0.8 * static_cast<double>(
         det_exp(static_cast<float>(iter * iter) / (-90.0f))));
     float probs[VMAX];
-    for (int i = 0; i < V; i++) {
+#pragma unroll
+    for (int i = 0; i < VMAX; i++) {
+        probs[i] = 0.0f;
+        if (i >= V) continue;
         float count = 0.0f;
         int count_false = 0;
         float tmpw = 0.0f;
@@ -1136,20 +1144,25 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
     }
     {
         float prob_sum = 0.0f;
-        for (int i = 0; i < V; ++i) prob_sum += probs[i];
+#pragma unroll
+        for (int i = 0; i < VMAX; ++i) if (i < V) prob_sum += probs[i];
         const float inv = 1.0f / prob_sum;
         float cum = 0.0f;
-        for (int i = 0; i < V; ++i) { cum = fmaf(probs[i], inv, cum); probs[i] = cum; }
+#pragma unroll
+        for (int i = 0; i < VMAX; ++i) if (i < V) { cum = fmaf(probs[i], inv, cum); probs[i] = cum; }
     }
     uint32_t vwp[4] = {0u, 0u, 0u, 0u};
     for (int sample = 0; sample < 15; ++sample) {
         const float rp = rs.uniform() - 1.1920928955078125e-07f;
-        for (int k = 0; k < V; ++k) {
-            if (probs[k] > rp) {
-                const uint32_t inc = 1u << ((k & 7) * 4);
-                if (k < 8) vwp[0] += inc; else if (k < 16) vwp[1] += inc; else if (k < 24) vwp[2] += inc; else vwp[3] += inc;
-                break;
-            }
+        // first view whose cumulative probability exceeds the draw (TransformPDFToCDF + :1190-1196)
+        int hit = -1;
+#pragma unroll
+        for (int k = VMAX - 1; k >= 0; --k)
+            if (k < V && probs[k] > rp) hit = k;
+        if (hit >= 0) {
+            const uint32_t inc = 1u << ((hit & 7) * 4);
+            if (hit < 8) vwp[0] += inc; else if (hit < 16) vwp[1] += inc; else if (hit < 24) vwp[2] += inc;
+            else vwp[3] += inc;
         }
     }
     uint32_t temp_sel = 0u;
