@@ -681,10 +681,10 @@ __device__ __forceinline__ void sort_small(float* d, int n) {
 }
 
 // ComputeMultiViewInitialCostandSelectedViews, ACMMP.cu:519-556
-template <int MODEL, int VB>
+template <int MODEL, int VB, int VMAXB = VB>
 __device__ float initial_cost(const KParams& kp, int px, int py, const Patch& pt, float4 ph, uint32_t* sel,
                               float* cvec = nullptr) {
-    constexpr int VMAX = VB < 8 ? VB : kMaxViews;            // pick_vb: V <= VB when VB < 8
+    constexpr int VMAX = VMAXB < 8 ? VMAXB : kMaxViews;      // pick_vb: V <= VMAXB when VMAXB < 8
     float cv[VMAX], cvc[VMAX];
     int nvalid = 0;
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
@@ -727,7 +727,15 @@ __device__ __forceinline__ float range_gauss(float x, float sigma) {
 // the common random branch does not carry the JBU loop's registers.
 enum InitBranch { kInitRandom = 0, kInitPlanar = 1, kInitUpsample = 2, kInitReuse = 3 };
 
-template <int MODEL, int VB, int BR>
+// k_init evaluates its (unstaged) NCCs two views at a time: with one lane per pixel every lane gathers
+// its own samples, and a wider chunk multiplies the wave's texel footprint past L1/L2 (measured: 1 view
+// 1.55 ms, 2 views 1.36 ms, 4 views 1.41 ms at 2000x1500, V = 4).
+#ifndef ACMMP_INIT_VB
+#define ACMMP_INIT_VB 2
+#endif
+constexpr int kInitVB = ACMMP_INIT_VB;
+
+template <int MODEL, int VB, int BR, int VMAXB>
 __global__ __launch_bounds__(256) void k_init(const KParams kp) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y * blockDim.y + threadIdx.y;
@@ -748,7 +756,7 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
         const float depth = fmaf(rs.uniform(), kp.depth_max - kp.depth_min, kp.depth_min);
         ph = random_normal(dc, rs);
         ph.w = dist_to_origin(dc, depth, ph);
-        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel, cvec);
+        cost = initial_cost<MODEL, VB, VMAXB>(kp, x, y, pt, ph, &sel, cvec);
     } else if (BR == kInitPlanar) {
         if (kp.mask[center] > 0 && kp.costs_rm[center] >= 0.1f) {
             const float perturbation = 0.02f;
@@ -764,7 +772,7 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
             const float depth = ph.w;
             ph.w = dist_to_origin(dc, depth, ph);
         }
-        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel, cvec);
+        cost = initial_cost<MODEL, VB, VMAXB>(kp, x, y, pt, ph, &sel, cvec);
     } else if (BR == kInitUpsample) {
         const float scale = static_cast<float>(1.0 * static_cast<double>(kp.scaled_cols) / static_cast<double>(kp.W));
         const float sigmad = 0.50f, sigmar = 25.5f;
@@ -798,16 +806,16 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
         normalize3(nx, ny, nz);
         const float4 cur = kp.planes_rm[center];
         uint32_t sel0;
-        kp.pre_rm[center] = initial_cost<MODEL, VB>(kp, x, y, pt, cur, &sel0);
+        kp.pre_rm[center] = initial_cost<MODEL, VB, VMAXB>(kp, x, y, pt, cur, &sel0);
         ph = to_ref(rc, make_float4(nx, ny, nz, 0.0f));
         ph.w = dist_to_origin(dc, cur.w, ph);
-        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel, cvec);
+        cost = initial_cost<MODEL, VB, VMAXB>(kp, x, y, pt, ph, &sel, cvec);
     } else {
         ph = kp.hier ? kp.scaled[center] : kp.planes_rm[center];
         ph = to_ref(rc, ph);
         const float depth = ph.w;
         ph.w = dist_to_origin(dc, depth, ph);
-        cost = initial_cost<MODEL, VB>(kp, x, y, pt, ph, &sel, cvec);
+        cost = initial_cost<MODEL, VB, VMAXB>(kp, x, y, pt, ph, &sel, cvec);
     }
     kp.plane_cs[colour][ci] = ph;
     kp.cost_cs[colour][ci] = cost;
@@ -1670,11 +1678,12 @@ hipError_t launch_init(const KParams& kp, hipStream_t s) {
     // branch order of ACMMP.cu:686-793
     const int br = (!kp.geom && !kp.hier) ? kInitRandom : kp.planar ? kInitPlanar : kp.upsample ? kInitUpsample
                                                                                                  : kInitReuse;
-    if (br == kInitRandom) ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC, kInitRandom><<<grd, blk, 0, s>>>(kp)));
-    else if (br == kInitPlanar) ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC, kInitPlanar><<<grd, blk, 0, s>>>(kp)));
+    if (br == kInitRandom) ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, kInitVB, kInitRandom, VBC><<<grd, blk, 0, s>>>(kp)));
+    else if (br == kInitPlanar)
+        ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, kInitVB, kInitPlanar, VBC><<<grd, blk, 0, s>>>(kp)));
     else if (br == kInitUpsample)
-        ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC, kInitUpsample><<<grd, blk, 0, s>>>(kp)));
-    else ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, VBC, kInitReuse><<<grd, blk, 0, s>>>(kp)));
+        ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, kInitVB, kInitUpsample, VBC><<<grd, blk, 0, s>>>(kp)));
+    else ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, kInitVB, kInitReuse, VBC><<<grd, blk, 0, s>>>(kp)));
     return hipGetLastError();
 }
 
