@@ -33,6 +33,8 @@ EXPORTS = [
     "acmmp_upload_depths_device", "acmmp_export_depth", "acmmp_device_alloc", "acmmp_device_free", "acmmp_memcpy",
     "acmmp_comm_unique_id", "acmmp_comm_create", "acmmp_comm_destroy", "acmmp_comm_broadcast",
     "acmmp_comm_allreduce_max",
+    "acmmp_fusion_create", "acmmp_fusion_set_view", "acmmp_fusion_run", "acmmp_fusion_last_error",
+    "acmmp_fusion_destroy",
 ]
 
 
@@ -93,13 +95,20 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_comm_destroy.argtypes = [vp]
     L.acmmp_comm_broadcast.argtypes = [vp, i32, vp, vp, vp]
     L.acmmp_comm_allreduce_max.argtypes = [vp, vp, i32]
+    L.acmmp_fusion_create.argtypes = [i32, i32, vp, C.POINTER(vp)]
+    L.acmmp_fusion_set_view.argtypes = [vp, i32, vp, vp, vp]
+    L.acmmp_fusion_run.argtypes = [vp, i32, i32, vp, vp, i32, vp]
+    L.acmmp_fusion_last_error.argtypes = [vp]
+    L.acmmp_fusion_destroy.argtypes = [vp]
     L.acmmp_planar_prior_host.argtypes = [vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]
     for name in EXPORTS:
         fn = getattr(L, name)
         if name not in ("acmmp_destroy", "acmmp_status_str", "acmmp_last_error", "acmmp_abi_version",
-                        "acmmp_depth_from_plane_param", "acmmp_comm_destroy"):
+                        "acmmp_depth_from_plane_param", "acmmp_comm_destroy", "acmmp_fusion_last_error",
+                        "acmmp_fusion_destroy"):
             fn.restype = i32
     L.acmmp_depth_from_plane_param.restype = C.c_float
+    L.acmmp_fusion_last_error.restype = C.c_char_p
     _lib = L
     return L
 
@@ -401,3 +410,50 @@ class Comm:
         if self.h:
             self.L.acmmp_comm_destroy(self.h)
             self.h = None
+
+
+# ---- GPU fusion (RunFusionCuda / SimpleFusionKernel, ACMMP.cu:1662-2105) ---------------------------
+
+class Fusion:
+    """Depth-map fusion on one GPU.  cams: CAMERA_DTYPE array, each rescaled to its depth map."""
+
+    def __init__(self, device: int, cams):
+        self.L = load_library()
+        self.cams = np.frombuffer(np.ascontiguousarray(cams, dtype=CAMERA_DTYPE).tobytes(), CAMERA_DTYPE).copy()
+        h = C.c_void_p()
+        _host_check(self.L.acmmp_fusion_create(device, len(self.cams), _p(self.cams), C.byref(h)), "fusion_create")
+        self.h = h
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.L.acmmp_fusion_last_error(self.h).decode()
+            raise AcmmpError(f"{what}: {self.L.acmmp_status_str(rc).decode()} ({msg})")
+
+    def set_view(self, view: int, depth, normals, bgr):
+        d = np.ascontiguousarray(depth, np.float32)
+        n = np.ascontiguousarray(normals, np.float32)
+        c = np.ascontiguousarray(bgr, np.uint8)
+        H, W = int(self.cams[view]["height"]), int(self.cams[view]["width"])
+        assert d.shape == (H, W) and n.shape == (H, W, 3) and c.shape == (H, W, 3)
+        self._check(self.L.acmmp_fusion_set_view(self.h, view, _p(d), _p(n), _p(c)), "fusion_set_view")
+
+    def run(self, ref: int, src_views) -> np.ndarray:
+        """Consistent points of reference view `ref`, (n, 9) float32 in pixel order."""
+        srcs = np.ascontiguousarray(src_views, np.int32)
+        n = C.c_int(0)
+        self.L.acmmp_fusion_run(self.h, ref, srcs.size, _p(srcs), None, 0, C.byref(n))
+        out = np.zeros((max(n.value, 1), 9), np.float32)
+        self._check(self.L.acmmp_fusion_run(self.h, ref, srcs.size, _p(srcs), _p(out), n.value, C.byref(n)),
+                    "fusion_run")
+        return out[:n.value]
+
+    def close(self):
+        if self.h:
+            self.L.acmmp_fusion_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

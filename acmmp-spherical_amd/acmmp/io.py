@@ -171,3 +171,46 @@ def scale_schedule(problems: list, max_num_downscale: int) -> list:
         out.append([p.cur_image_size for p in ps])
         scale -= 1
     return out
+
+
+def write_ply(path: str, points: np.ndarray) -> None:
+    """StoreColorPlyFileBinaryPointCloud (ACMMP.cpp:481-534).  points: (n, 9) float32 rows
+    x y z nx ny nz c0 c1 c2 as SimpleFusionKernel stores them (c0 = the texture's .z channel);
+    the writer emits red = (char)(int)c2, green = (char)(int)c1, blue = (char)(int)c0 and zeroes
+    coordinates that are not finite (the FLT_MAX tests of :508-512, including the z >= -FLT_MAX quirk)."""
+    p = np.ascontiguousarray(points, np.float32).reshape(-1, 9)
+    n = p.shape[0]
+    X = p[:, 0:3].copy()
+    fmax = np.float32(np.finfo(np.float32).max)
+    bad = ~((X[:, 0] < fmax) & (X[:, 0] > -fmax)) | ~((X[:, 1] < fmax) & (X[:, 1] > -fmax)) | \
+        ~((X[:, 2] < fmax) & (X[:, 2] >= -fmax))
+    X[bad] = 0.0
+    rec = np.zeros(n, dtype=[("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
+                             ("r", "u1"), ("g", "u1"), ("b", "u1")])
+    rec["x"], rec["y"], rec["z"] = X[:, 0], X[:, 1], X[:, 2]
+    rec["nx"], rec["ny"], rec["nz"] = p[:, 3], p[:, 4], p[:, 5]
+
+    def to_char(v):   # (char)(int)v: truncation toward zero, then the low byte
+        with np.errstate(invalid="ignore"):
+            iv = np.where(np.isfinite(v), np.trunc(v), 0).astype(np.int64)
+        return (iv & 0xFF).astype(np.uint8)
+    rec["r"], rec["g"], rec["b"] = to_char(p[:, 8]), to_char(p[:, 7]), to_char(p[:, 6])
+    header = ("ply\nformat binary_little_endian 1.0\n"
+              f"element vertex {n}\n"
+              "property float x\nproperty float y\nproperty float z\n"
+              "property float nx\nproperty float ny\nproperty float nz\n"
+              "property uchar red\nproperty uchar green\nproperty uchar blue\nend_header\n")
+    with open(path, "wb") as f:
+        f.write(header.encode("ascii"))
+        f.write(rec.tobytes())
+
+
+def read_ply(path: str) -> np.ndarray:
+    """Reader for write_ply's layout (tests): structured array x y z nx ny nz r g b."""
+    with open(path, "rb") as f:
+        data = f.read()
+    end = data.index(b"end_header\n") + len(b"end_header\n")
+    n = int([l for l in data[:end].decode().splitlines() if l.startswith("element vertex")][0].split()[2])
+    dt = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
+                   ("r", "u1"), ("g", "u1"), ("b", "u1")])
+    return np.frombuffer(data[end:end + n * dt.itemsize], dtype=dt).copy()

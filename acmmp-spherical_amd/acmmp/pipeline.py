@@ -44,6 +44,7 @@ class Dataset:
     cameras: dict
     problems: list
     folder: str | None = None
+    colors: dict | None = None        # optional BGR uint8 images for fusion (IMREAD_COLOR); grey otherwise
 
 
 def read_gray(path: str) -> np.ndarray:
@@ -56,16 +57,25 @@ def read_gray(path: str) -> np.ndarray:
         return np.asarray(im.convert("L"), dtype=np.float32).copy()
 
 
-def load_dataset(dense_folder: str) -> Dataset:
+def read_bgr(path: str) -> np.ndarray:
+    """cv::imread(IMREAD_COLOR): 8-bit BGR."""
+    from PIL import Image
+    with Image.open(path) as im:
+        return np.asarray(im.convert("RGB"), dtype=np.uint8)[..., ::-1].copy()
+
+
+def load_dataset(dense_folder: str, with_colors: bool = False) -> Dataset:
     problems = io.read_pair_list(dense_folder)
-    images, cameras = {}, {}
+    images, cameras, colors = {}, {}, ({} if with_colors else None)
     for p in problems:
         i = p.ref_image_id
         images[i] = read_gray(os.path.join(dense_folder, "images", f"{i:08d}.jpg"))
+        if with_colors:
+            colors[i] = read_bgr(os.path.join(dense_folder, "images", f"{i:08d}.jpg"))
         cam = io.read_camera(os.path.join(dense_folder, "cams", f"{i:08d}_cam.txt"))
         cam["height"], cam["width"] = images[i].shape
         cameras[i] = cam
-    return Dataset(images, cameras, problems, dense_folder)
+    return Dataset(images, cameras, problems, dense_folder, colors)
 
 
 def resize_linear(img: np.ndarray, new_cols: int, new_rows: int) -> np.ndarray:
@@ -92,6 +102,75 @@ def resize_linear(img: np.ndarray, new_cols: int, new_rows: int) -> np.ndarray:
     ys0, ys1, by0, by1 = taps(new_rows, rows)
     h = (src[:, xs0] * ax0 + src[:, xs1] * ax1).astype(np.float32)
     return (h[ys0] * by0[:, None] + h[ys1] * by1[:, None]).astype(np.float32)
+
+
+def resize_linear_u8(img: np.ndarray, new_cols: int, new_rows: int) -> np.ndarray:
+    """cv::resize(INTER_LINEAR) of an 8-bit image (any channel count): OpenCV's fixed-point path --
+    coefficients rounded to 11 bits, horizontal sums kept as ints, vertical pass
+    (b0 * S0 + b1 * S1 + 2^21) >> 22.  SIMD-path details are not pinned."""
+    src = np.asarray(img, np.uint8)
+    if src.ndim == 2:
+        return resize_linear_u8(src[..., None], new_cols, new_rows)[..., 0]
+    rows, cols = src.shape[:2]
+
+    def taps(dsize, ssize):
+        scale = ssize / dsize
+        d = np.arange(dsize, dtype=np.float64)
+        f = ((d + 0.5) * scale - 0.5).astype(np.float32)
+        s0 = np.floor(f).astype(np.int64)
+        f = (f - s0.astype(np.float32)).astype(np.float32)
+        lo = s0 < 0
+        f[lo], s0[lo] = 0.0, 0
+        hi = s0 >= ssize - 1
+        f[hi], s0[hi] = 0.0, ssize - 1
+        s1 = np.minimum(s0 + 1, ssize - 1)
+        a0 = np.rint((np.float32(1.0) - f) * np.float32(2048.0)).astype(np.int64)
+        a1 = np.rint(f * np.float32(2048.0)).astype(np.int64)
+        return s0, s1, a0, a1
+
+    xs0, xs1, ax0, ax1 = taps(new_cols, cols)
+    ys0, ys1, by0, by1 = taps(new_rows, rows)
+    S = src.astype(np.int64)
+    h = S[:, xs0, :] * ax0[None, :, None] + S[:, xs1, :] * ax1[None, :, None]
+    v = h[ys0] * by0[:, None, None] + h[ys1] * by1[:, None, None]
+    return np.clip((v + (1 << 21)) >> 22, 0, 255).astype(np.uint8)
+
+
+def rescale_image_and_camera(bgr: np.ndarray, depth_shape, cam: np.ndarray):
+    """RescaleImageAndCamera (ACMMP.cpp:213-246): camera size := depth size; image resized to it
+    (INTER_LINEAR) and (cx, cy) / K scaled when the sizes differ."""
+    cam = np.array(cam, copy=True)
+    rows, cols = depth_shape
+    cam["width"], cam["height"] = cols, rows
+    if bgr.shape[0] == rows and bgr.shape[1] == cols:
+        return np.array(bgr, copy=True), cam
+    sx = np.float32(cols) / np.float32(bgr.shape[1])
+    sy = np.float32(rows) / np.float32(bgr.shape[0])
+    out = resize_linear_u8(bgr, cols, rows)
+    if int(cam["model"]) == types.SPHERE:
+        cam["params"][1] = np.float32(cam["params"][1] * sx)
+        cam["params"][2] = np.float32(cam["params"][2] * sy)
+    else:
+        K = cam["K"]
+        K[0] = np.float32(K[0] * sx); K[2] = np.float32(K[2] * sx)
+        K[4] = np.float32(K[4] * sy); K[5] = np.float32(K[5] * sy)
+        cam["K"] = K
+    return out, cam
+
+
+def fusion_inputs(ds: "Dataset", store, problems):
+    """RunFusionCuda's loading loop (ACMMP.cu:1833-1886): per view the final depth map
+    (depths_geom), normals and the colour image rescaled to the depth size, with its camera."""
+    cams, depths, normals, colours = [], [], [], []
+    for p in problems:
+        i = p.ref_image_id
+        d = store.get("depths_geom", i)
+        n = store.get("normals", i)
+        bgr = ds.colors[i] if ds.colors and i in ds.colors else \
+            np.repeat(np.clip(np.round(ds.images[i]), 0, 255).astype(np.uint8)[..., None], 3, axis=2)
+        img, cam = rescale_image_and_camera(bgr, d.shape, ds.cameras[i])
+        cams.append(cam); depths.append(d); normals.append(n); colours.append(img)
+    return np.array(cams, dtype=types.CAMERA_DTYPE), depths, normals, colours
 
 
 def scale_view(image: np.ndarray, cam: np.ndarray, max_image_size: int):
@@ -216,6 +295,7 @@ class Pipeline:
         if order not in ("reference", "snapshot"):
             raise ValueError(order)
         self.order = order
+        self.device = device
         self.engine = engine if engine is not None else capi.Context(device)
         gpu = isinstance(self.engine, capi.Context)
         self.store = ViewStore(device if (gpu if use_device_store is None else use_device_store) else None)
@@ -236,7 +316,7 @@ class Pipeline:
     def my_problems(self):
         return [i for i in range(len(self.problems)) if self.owner(i) == self.rank]
 
-    # -- the schedule (main.cpp:392-482, fusion excluded)
+    # -- the schedule (main.cpp:392-482); fusion is run_fusion()
     def run(self):
         sizes = {p.ref_image_id: self.ds.images[p.ref_image_id].shape for p in self.problems}
         max_num_downscale = io.compute_multiscale_settings(self.problems, sizes, self.max_image_size,
@@ -381,6 +461,42 @@ class Pipeline:
             io.write_dmb(os.path.join(d, "costs.dmb"), costs)
         return planes, costs
 
+    # -- RunFusionCuda (ACMMP.cu:1817-2105), after the last pass
+    def run_fusion(self, fusion_factory=None, ply_path: str | None = None):
+        """Fuse every view's final depth map on this rank's GPU (rank 0 when sharded: the other ranks
+        broadcast their normals to it first; depths_geom were exchanged after the last pass).
+        Returns the (n, 9) points and writes ACMMP/ACMM_model_cuda_5.ply when an output folder is set."""
+        if self.world > 1:
+            views = [p.ref_image_id for p in self.problems]
+            owners = {self.problems[i].ref_image_id: self.owner(i) for i in range(len(self.problems))}
+            for v in views:
+                shape = (*self._pass_shape(v), 3)
+                if owners[v] == self.rank and self.store.device is not None:
+                    self.store.device_map("normals", v, shape).upload(self.store.get("normals", v))
+                self.store.shapes[("normals", v)] = shape
+            self.exchange.share("normals", views, owners, self.store)
+            if self.rank != 0:
+                return None
+        cams, depths, normals, colours = fusion_inputs(self.ds, self.store, self.problems)
+        make = fusion_factory or (lambda c: capi.Fusion(self.device, c))
+        fu = make(cams)
+        for k in range(len(cams)):
+            fu.set_view(k, depths[k], normals[k], colours[k])
+        index = {p.ref_image_id: k for k, p in enumerate(self.problems)}
+        pts = []
+        for k, p in enumerate(self.problems):
+            srcs = [index.get(s, -1) for s in p.src_image_ids][:32]            # ACMMP.cu:2010-2023
+            pts.append(fu.run(k, srcs))
+        if hasattr(fu, "close"):
+            fu.close()
+        points = np.concatenate(pts, 0) if pts else np.zeros((0, 9), np.float32)
+        path = ply_path or (os.path.join(self.out_folder, "ACMMP", "ACMM_model_cuda_5.ply") if self.out_folder else None)
+        if path:
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            io.write_ply(path, points)
+        self.fused = points
+        return points
+
     # -- JointBilateralUpsampling (main.cpp:212-238) + RunJBU (ACMMP.cpp:1071-1122)
     def joint_bilateral_upsampling(self, idx, acmmp_size):
         ref = self.problems[idx].ref_image_id
@@ -453,7 +569,8 @@ def write_dense_folder(folder: str, ds: Dataset, pairs=None, quality: int = 95):
 
 
 def main(argv=None):
-    """`python -m acmmp.pipeline DENSE_FOLDER` -- the reference's `ACMMP dense_folder` without fusion.
+    """`python -m acmmp.pipeline DENSE_FOLDER` -- the reference's `ACMMP dense_folder` (main.cpp:369-489):
+    the multi-scale schedule, then RunFusionCuda into ACMMP/ACMM_model_cuda_5.ply.
     Under torchrun (WORLD_SIZE > 1) every rank drives GPU LOCAL_RANK, views are sharded and the
     depth maps are exchanged over RCCL between passes (snapshot order)."""
     import argparse
@@ -465,19 +582,25 @@ def main(argv=None):
     ap.add_argument("--order", choices=["reference", "snapshot"], default=None)
     ap.add_argument("--geom-iterations", type=int, default=2)
     ap.add_argument("--no-dmb", action="store_true", help="keep results in memory only")
+    ap.add_argument("--no-fusion", action="store_true", help="skip RunFusionCuda")
     a = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     device = int(os.environ.get("LOCAL_RANK", "0"))
     order = a.order or ("reference" if world == 1 else "snapshot")
-    ds = load_dataset(a.dense_folder)
+    ds = load_dataset(a.dense_folder, with_colors=not a.no_fusion)
     exchange = rcclexchange_from_env(device)
     t0 = time.perf_counter()
     pipe = Pipeline(ds, exchange=exchange, device=device, seed=a.seed, order=order,
                     geom_iterations=a.geom_iterations, out_folder=None if a.no_dmb else a.dense_folder,
                     log=lambda *m: print(*m, flush=True)).run()
+    n_points = None
+    if not a.no_fusion:
+        pts = pipe.run_fusion(ply_path=os.path.join(a.dense_folder, "ACMMP", "ACMM_model_cuda_5.ply"))
+        n_points = None if pts is None else int(pts.shape[0])
     dt = time.perf_counter() - t0
     print(json.dumps({"rank": pipe.rank, "world": pipe.world, "views": len(pipe.my_problems()),
-                      "passes": [p.name for p in pipe.passes], "seconds": round(dt, 3)}), flush=True)
+                      "passes": [p.name for p in pipe.passes], "fused_points": n_points,
+                      "seconds": round(dt, 3)}), flush=True)
     exchange.close()
     return 0
 

@@ -141,6 +141,7 @@ def sphere_scene(width: int = 2000, height: int = 1000, n_src: int = 4, seed: in
     dmin = 0.5 * float(np.min(half))
     dmax = 1.2 * float(np.linalg.norm(half))
     imgs, cams, gt = [], [], None
+    gt_depths, gt_normals = [], []
     ppu = width / (2 * np.pi * float(np.mean(half)))   # pixels per world unit at mean distance
     fmin, fmax = 2 * np.pi * ppu / 30.0, 2 * np.pi * ppu / 6.0
     for C, R in zip(centers, rots):
@@ -156,7 +157,15 @@ def sphere_scene(width: int = 2000, height: int = 1000, n_src: int = 4, seed: in
                                 width=width, height=height, depth_min=dmin, depth_max=dmax))
         if gt is None:
             gt = t.astype(np.float32)
-    return Scene(imgs, np.array(cams), gt, "sphere", {})
+        gt_depths.append(t.astype(np.float32))
+        # world-frame normal of the face hit, facing the camera (the room is seen from inside)
+        axis = np.argmin(np.where(d > 0, (half - C) / np.where(d == 0, 1, d),
+                                  np.where(d < 0, (-half - C) / np.where(d == 0, 1, d), np.inf)), axis=-1)
+        n = np.zeros(d.shape, np.float32)
+        sgn = np.take_along_axis(d, axis[..., None], -1)[..., 0]
+        np.put_along_axis(n, axis[..., None], (-np.sign(sgn))[..., None].astype(np.float32), -1)
+        gt_normals.append(n)
+    return Scene(imgs, np.array(cams), gt, "sphere", {"gt_depths": gt_depths, "gt_normals": gt_normals})
 
 
 def depth_accuracy(depth: np.ndarray, gt: np.ndarray, rel: float = 0.01, mask=None) -> float:

@@ -112,6 +112,25 @@ float neg_dot3(float a0, float a1, float a2, float b0, float b1, float b2) {
 
 }  // namespace
 
+DevCam acmmp::make_devcam(const acmmp_camera& s) {
+    DevCam d{};
+    d.model = s.model; d.W = s.width; d.H = s.height; d.img_pitch = s.width + 2;
+    std::memcpy(d.R, s.R, sizeof d.R);
+    std::memcpy(d.t, s.t, sizeof d.t);
+    std::memcpy(d.K, s.K, sizeof d.K);
+    d.cx = s.params[1]; d.cy = s.params[2];
+    d.inv_fx = 1.0f / s.K[0];
+    d.inv_fy = 1.0f / s.K[4];
+    d.invW = 1.0f / static_cast<float>(s.width);
+    d.Wf = static_cast<float>(s.width);
+    d.Hf = static_cast<float>(s.height);
+    d.C[0] = neg_dot3(s.R[0], s.R[3], s.R[6], s.t[0], s.t[1], s.t[2]);
+    d.C[1] = neg_dot3(s.R[1], s.R[4], s.R[7], s.t[0], s.t[1], s.t[2]);
+    d.C[2] = neg_dot3(s.R[2], s.R[5], s.R[8], s.t[0], s.t[1], s.t[2]);
+    d.dep_w = 1; d.dep_h = 1;
+    return d;
+}
+
 extern "C" {
 
 int acmmp_abi_version(void) { return ACMMP_ABI_VERSION; }
@@ -187,6 +206,7 @@ acmmp_status acmmp_set_params(acmmp_ctx* c, const acmmp_params* p) {
     return ACMMP_OK;
 }
 
+
 acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images, const size_t* pitch_bytes,
                                 const acmmp_camera* cams) {
     if (!c || !images || !cams) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
@@ -241,19 +261,7 @@ acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images,
     for (int i = 0; i < n; ++i) {
         const acmmp_camera& s = cams[i];
         DevCam& d = c->dcams[i];
-        d.model = s.model; d.W = s.width; d.H = s.height; d.img_pitch = s.width + 2;
-        std::memcpy(d.R, s.R, sizeof d.R);
-        std::memcpy(d.t, s.t, sizeof d.t);
-        std::memcpy(d.K, s.K, sizeof d.K);
-        d.cx = s.params[1]; d.cy = s.params[2];
-        d.inv_fx = 1.0f / s.K[0];
-        d.inv_fy = 1.0f / s.K[4];
-        d.invW = 1.0f / static_cast<float>(s.width);
-        d.Wf = static_cast<float>(s.width);
-        d.Hf = static_cast<float>(s.height);
-        d.C[0] = neg_dot3(s.R[0], s.R[3], s.R[6], s.t[0], s.t[1], s.t[2]);
-        d.C[1] = neg_dot3(s.R[1], s.R[4], s.R[7], s.t[0], s.t[1], s.t[2]);
-        d.C[2] = neg_dot3(s.R[2], s.R[5], s.R[8], s.t[0], s.t[1], s.t[2]);
+        d = make_devcam(s);
         d.img_off = off[i];
         d.img_bytes = static_cast<int>(4LL * (s.width + 2) * (s.height + 2));
         d.dep_off = 0; d.dep_w = 1; d.dep_h = 1;

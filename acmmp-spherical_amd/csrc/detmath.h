@@ -171,6 +171,9 @@ ACMMP_HD float det_atan2(float y, float x) {
 
 ACMMP_HD float det_rsqrt(float x) { return 1.0f / sqrtf(x); }
 
+// hypotf (SimpleFusionKernel, ACMMP.cu:1750, 1790): sqrt(x*x + y*y) with the contraction rule.
+ACMMP_HD float det_hypot(float x, float y) { return sqrtf(fmaf(y, y, x * x)); }
+
 ACMMP_HD float dot3(float a0, float a1, float a2, float b0, float b1, float b2) {
     return fmaf(a2, b2, fmaf(a1, b1, a0 * b0));
 }

@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "acmmp.h"
+
 namespace acmmp {
 
 constexpr int kPinhole = 0;
@@ -100,6 +102,15 @@ struct KParams {
 };
 
 // Per-half-sweep output buffers of the colour being updated.
+// One view of the fusion set (device pointers): depth (W x H), normals (3 floats per pixel, world
+// frame as normals.dmb holds them), colour as the reference's float RGBA texture (4 per pixel, /255).
+struct FuseView {
+    const float* depth;
+    const float* normal;
+    const float* rgba;
+    int W, H;
+};
+
 struct SweepOut {
     float4* plane;
     float* cost;
@@ -113,6 +124,16 @@ hipError_t launch_init(const KParams& kp, hipStream_t s);
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s,
                             hipEvent_t* ev = nullptr);
 hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s);
+// Reference Camera -> device camera (derived constants computed as DESIGN.md §2.3 says), capi.cpp.
+DevCam make_devcam(const acmmp_camera& cam);
+
+// SimpleFusionKernel (ACMMP.cu:1662-1814) for reference view `ref` + compaction in pixel order:
+// out_dense/flags are P-sized scratch, block_counts ceil(P/256) ints.
+hipError_t launch_fuse(int model, const DevCam* cams, const FuseView* views, int ref, int W, int H, const int* srcs,
+                       int n_src, float* out_dense, int* flags, int* block_counts, hipStream_t s);
+// block_counts: valid pixels per 256-pixel chunk (written by launch_fuse); block_offsets: their prefix.
+hipError_t launch_fuse_compact(int W, int H, const float* out_dense, const int* flags, const int* block_offsets,
+                               float* out, hipStream_t s);
 hipError_t launch_export_depth(const float4* planes, long long P, float* dst, hipStream_t s);
 hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int sw, int sh, int imagescale,
                       float* out, hipStream_t s);

@@ -148,13 +148,15 @@ __device__ __forceinline__ float asin_proj(float x) {
 }
 
 // ProjectonCamera_cu, ACMMP.cu:602-644 (Cam: DevCam in any address space)
-template <int MODEL, typename Cam>
+template <int MODEL, typename Cam, bool EXACT_DEPTH = false>
 __device__ __forceinline__ void project(Cam& c, float3 P, float& ox, float& oy, float& depth) {
     const float tx = dot3(c.R[0], c.R[1], c.R[2], P.x, P.y, P.z) + c.t[0];
     const float ty = dot3(c.R[3], c.R[4], c.R[5], P.x, P.y, P.z) + c.t[1];
     const float tz = dot3(c.R[6], c.R[7], c.R[8], P.x, P.y, P.z) + c.t[2];
     if (MODEL == kSphere) {
-        const float d = sqrt_proj(dot3(tx, ty, tz, tx, ty, tz));
+        // sqrt_proj differs from sqrtf only below 2^-96, where the point is replaced by the principal
+        // point; callers that use the returned depth (fusion) ask for the IEEE square root
+        const float d = EXACT_DEPTH ? sqrtf(dot3(tx, ty, tz, tx, ty, tz)) : sqrt_proj(dot3(tx, ty, tz, tx, ty, tz));
         depth = d;
         const float neg_lat = asin_proj(ty / d);
         const float lon = det_atan2(tx, tz);
@@ -1723,9 +1725,145 @@ hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s) {
     return hipGetLastError();
 }
 
+
+// ------------------------------------------------------------------ kernel: fusion
+
+// tex2D<float4>(linear filter, unnormalised (c, r)) at an integer texel index WITHOUT the +0.5
+// (ACMMP.cu:1690, 1768): the footprint is texels (c-1, c) x (r-1, r), both weights 0.5, clamped
+// (wrap is undefined for unnormalised coordinates and acts as clamp).  fp32 fused lerps.
+__device__ __forceinline__ float4 fuse_colour(const float* rgba, int W, int H, int c, int r) {
+    const int x0 = c - 1 < 0 ? 0 : c - 1, x1 = c > W - 1 ? W - 1 : c;
+    const int y0 = r - 1 < 0 ? 0 : r - 1, y1 = r > H - 1 ? H - 1 : r;
+    const float4 t00 = reinterpret_cast<const float4*>(rgba)[static_cast<long long>(y0) * W + x0];
+    const float4 t10 = reinterpret_cast<const float4*>(rgba)[static_cast<long long>(y0) * W + x1];
+    const float4 t01 = reinterpret_cast<const float4*>(rgba)[static_cast<long long>(y1) * W + x0];
+    const float4 t11 = reinterpret_cast<const float4*>(rgba)[static_cast<long long>(y1) * W + x1];
+    auto lerp = [](float a, float b) { return fmaf(0.5f, b - a, a); };
+    const float4 top = make_float4(lerp(t00.x, t10.x), lerp(t00.y, t10.y), lerp(t00.z, t10.z), lerp(t00.w, t10.w));
+    const float4 bot = make_float4(lerp(t01.x, t11.x), lerp(t01.y, t11.y), lerp(t01.z, t11.z), lerp(t01.w, t11.w));
+    return make_float4(lerp(top.x, bot.x), lerp(top.y, bot.y), lerp(top.z, bot.z), lerp(top.w, bot.w));
+}
+
+// SimpleFusionKernel, ACMMP.cu:1662-1814: per reference pixel, the source views whose depth
+// reprojects within 1 px, 1% depth and 0.149 rad of normal; >= 3 consistent (the reference
+// included) -> averaged point, normal and colour.  out: 9 floats per pixel (x y z nx ny nz c0 c1 c2,
+// c0 = 255 * texture .z as the reference stores it).
+template <int MODEL>
+__global__ void k_fuse(const DevCam* __restrict__ cams, const FuseView* __restrict__ views, int ref, int W, int H,
+                       const int* __restrict__ srcs, int n_src, float* __restrict__ out, int* __restrict__ flags) {
+    const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int r = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const bool inside = c < W && r < H;
+    int valid = 0;
+    const long long idx = static_cast<long long>(r) * W + c;
+    if (inside) {
+        const DevCam& rc = cams[ref];
+        const FuseView rv = views[ref];
+        const float ref_depth = rv.depth[idx];
+        if (!(ref_depth <= 0.0f)) {
+            const float3 X = world_point<MODEL>(rc, static_cast<float>(c), static_cast<float>(r), ref_depth);
+            const float rn0 = rv.normal[3 * idx], rn1 = rv.normal[3 * idx + 1], rn2 = rv.normal[3 * idx + 2];
+            const float4 rcol = fuse_colour(rv.rgba, W, H, c, r);
+            float ps0 = X.x, ps1 = X.y, ps2 = X.z;
+            float ns0 = rn0, ns1 = rn1, ns2 = rn2;
+            float cs0 = rcol.z * 255.0f, cs1 = rcol.y * 255.0f, cs2 = rcol.x * 255.0f;
+            int n = 1;
+            for (int j = 0; j < n_src; ++j) {
+                const int si = srcs[j];
+                if (si < 0) continue;
+                const DevCam& sc = cams[si];
+                const FuseView sv = views[si];
+                float px, py, pd;
+                project<MODEL, const DevCam, true>(sc, X, px, py, pd);
+                const int src_c = f2i_sat(px + 0.5f), src_r = f2i_sat(py + 0.5f);
+                if (src_c < 0 || src_c >= sc.W || src_r < 0 || src_r >= sc.H) continue;
+                const long long sidx = static_cast<long long>(src_r) * sv.W + src_c;
+                const float sd = sv.depth[sidx];
+                if (sd <= 0.0f) continue;
+                const float3 Xs = world_point<MODEL>(sc, static_cast<float>(src_c), static_cast<float>(src_r), sd);
+                float qx, qy, qd;
+                project<MODEL, const DevCam, true>(rc, Xs, qx, qy, qd);
+                const float err = det_hypot(static_cast<float>(c) - qx, static_cast<float>(r) - qy);
+                const float rel = fabsf(pd - sd) / sd;
+                const float sn0 = sv.normal[3 * sidx], sn1 = sv.normal[3 * sidx + 1], sn2 = sv.normal[3 * sidx + 2];
+                float dp = dot3(rn0, rn1, rn2, sn0, sn1, sn2);
+                dp = fmaxf(-1.0f, fminf(1.0f, dp));
+                const float ang = det_acos(dp);
+                if (err < 1.0f && rel < 0.01f && ang < 0.149f) {
+                    ps0 += Xs.x; ps1 += Xs.y; ps2 += Xs.z;
+                    ns0 += sn0; ns1 += sn1; ns2 += sn2;
+                    const float4 scol = fuse_colour(sv.rgba, sv.W, sv.H, src_c, src_r);
+                    cs0 = fmaf(scol.z, 255.0f, cs0);
+                    cs1 = fmaf(scol.y, 255.0f, cs1);
+                    cs2 = fmaf(scol.x, 255.0f, cs2);
+                    ++n;
+                }
+            }
+            if (n >= 3) {
+                const float fn = static_cast<float>(n);
+                float* o = out + 9 * idx;
+                o[0] = ps0 / fn; o[1] = ps1 / fn; o[2] = ps2 / fn;
+                float a0 = ns0 / fn, a1 = ns1 / fn, a2 = ns2 / fn;
+                const float len = det_hypot(det_hypot(a0, a1), a2);
+                if (len > 0.0f) { a0 /= len; a1 /= len; a2 /= len; }
+                o[3] = a0; o[4] = a1; o[5] = a2;
+                o[6] = cs0 / fn; o[7] = cs1 / fn; o[8] = cs2 / fn;
+                valid = 1;
+            }
+        }
+        flags[idx] = valid;
+    }
+}
+
+// counts of valid pixels per 256-pixel chunk of the row-major image
+__global__ void k_fuse_count(const int* __restrict__ flags, long long P, int* __restrict__ counts) {
+    const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+    const int f = i < P ? flags[i] : 0;
+    const int n = __syncthreads_count(f);
+    if (threadIdx.x == 0) counts[blockIdx.x] = n;
+}
+
+// scatter the valid pixels of each chunk to offsets[chunk] + rank within the chunk (pixel order)
+__global__ void k_fuse_scatter(const float* __restrict__ dense, const int* __restrict__ flags, long long P,
+                               const int* __restrict__ offsets, float* __restrict__ out) {
+    __shared__ int wave_tot[4];
+    const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+    const int f = i < P ? flags[i] : 0;
+    const unsigned long long b = __ballot(f);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int below = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_tot[wave] = __popcll(b);
+    __syncthreads();
+    int base = offsets[blockIdx.x];
+    for (int w = 0; w < wave; ++w) base += wave_tot[w];
+    if (f) {
+        float* o = out + 9ll * (base + below);
+        const float* d = dense + 9 * i;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) o[k] = d[k];
+    }
+}
+
 __global__ void k_export_depth(const float4* __restrict__ planes, long long P, float* __restrict__ dst) {
     const long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i < P) dst[i] = planes[i].w;
+}
+
+hipError_t launch_fuse(int model, const DevCam* cams, const FuseView* views, int ref, int W, int H, const int* srcs,
+                       int n_src, float* out_dense, int* flags, int* block_counts, hipStream_t s) {
+    dim3 grd(cdiv(W, 16), cdiv(H, 16));
+    if (model == kSphere) k_fuse<kSphere><<<grd, 256, 0, s>>>(cams, views, ref, W, H, srcs, n_src, out_dense, flags);
+    else k_fuse<kPinhole><<<grd, 256, 0, s>>>(cams, views, ref, W, H, srcs, n_src, out_dense, flags);
+    const long long P = static_cast<long long>(W) * H;
+    k_fuse_count<<<static_cast<unsigned>((P + 255) / 256), 256, 0, s>>>(flags, P, block_counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_fuse_compact(int W, int H, const float* out_dense, const int* flags, const int* block_offsets,
+                               float* out, hipStream_t s) {
+    const long long P = static_cast<long long>(W) * H;
+    k_fuse_scatter<<<static_cast<unsigned>((P + 255) / 256), 256, 0, s>>>(out_dense, flags, P, block_offsets, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_export_depth(const float4* planes, long long P, float* dst, hipStream_t s) {

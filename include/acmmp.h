@@ -78,6 +78,7 @@ typedef enum acmmp_status {
 
 typedef struct acmmp_ctx acmmp_ctx;
 typedef struct acmmp_comm acmmp_comm;
+typedef struct acmmp_fusion acmmp_fusion;
 #define ACMMP_COMM_ID_BYTES 128
 
 /* ACMMP::ACMMP() (ACMMP.cpp:99) + cudaSetDevice (main.cpp:77).  `device` is a HIP
@@ -187,6 +188,23 @@ acmmp_status acmmp_comm_broadcast(acmmp_comm *comm, int n, void *const *bufs, co
 
 /* Element-wise max over ranks of n host doubles (timing reductions); synchronous. */
 acmmp_status acmmp_comm_allreduce_max(acmmp_comm *comm, double *vals, int n);
+
+/* ---- GPU depth-map fusion (RunFusionCuda + SimpleFusionKernel, ACMMP.cu:1662-2105) -------------
+ * One object per fusion run.  cams[i] is view i's camera already rescaled to its depth map
+ * (RescaleImageAndCamera, ACMMP.cpp:213-246).  set_view uploads what the reference puts in textures:
+ * the depth map (H x W), world-frame normals (3 floats per pixel, normals.dmb) and the colour image
+ * rescaled to the depth size (3 bytes per pixel, OpenCV BGR order).  run fuses reference view `ref`
+ * against src_views (indices into the set, -1 = missing, at most 32) and returns the consistent
+ * points in pixel order, 9 floats each: x y z nx ny nz c0 c1 c2 (colour slots as the kernel stores them,
+ * ACMMP.cu:1706-1708; StoreColorPlyFileBinaryPointCloud writes c2, c1, c0 as red, green, blue).
+ * When `cap` is too small *n_points holds the count and ACMMP_ERR_INVALID_ARGUMENT is returned. */
+acmmp_status acmmp_fusion_create(int device, int n_views, const acmmp_camera *cams, acmmp_fusion **out);
+acmmp_status acmmp_fusion_set_view(acmmp_fusion *f, int view, const float *depth, const float *normals,
+                                   const uint8_t *bgr);
+acmmp_status acmmp_fusion_run(acmmp_fusion *f, int ref, int n_src, const int *src_views, float *points, int cap,
+                              int *n_points);
+const char *acmmp_fusion_last_error(const acmmp_fusion *f);
+void acmmp_fusion_destroy(acmmp_fusion *f);
 
 /* ---- planar-prior host side (no GPU; ACMMP.cpp:904-1011, main.cpp:113-181) ---------------
  * Host restatements of the reference's planar-prior helpers, so a caller can run ProcessProblem's

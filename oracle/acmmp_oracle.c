@@ -1110,6 +1110,96 @@ void or_world_point(const or_camera *cam, float x, float y, float depth, float o
     out[0] = r.x; out[1] = r.y; out[2] = r.z;
 }
 
+/* ---- fusion: SimpleFusionKernel, ACMMP.cu:1662-1814 ------------------------------------- */
+
+/* hypotf as a fixed definition: sqrt(x*x + y*y) under the contraction rule */
+static inline float fuse_hypot(float x, float y) { return sqrtf(fmaf(y, y, x * x)); }
+
+/* tex2D<float4>(linear, unnormalised) at integer (c, r) -- no +0.5 (ACMMP.cu:1690): texels
+ * (c-1, c) x (r-1, r), weights 0.5, clamped; fused fp32 lerps */
+static void fuse_colour(const float *rgba, int W, int H, int c, int r, float out[4])
+{
+    const int x0 = c - 1 < 0 ? 0 : c - 1, x1 = c > W - 1 ? W - 1 : c;
+    const int y0 = r - 1 < 0 ? 0 : r - 1, y1 = r > H - 1 ? H - 1 : r;
+    for (int k = 0; k < 4; ++k) {
+        const float t00 = rgba[4 * ((size_t)y0 * W + x0) + k], t10 = rgba[4 * ((size_t)y0 * W + x1) + k];
+        const float t01 = rgba[4 * ((size_t)y1 * W + x0) + k], t11 = rgba[4 * ((size_t)y1 * W + x1) + k];
+        const float top = fmaf(0.5f, t10 - t00, t00), bot = fmaf(0.5f, t11 - t01, t01);
+        out[k] = fmaf(0.5f, bot - top, top);
+    }
+}
+
+int32_t or_fuse(int32_t n, const or_camera *cams, const float *const *depths, const float *const *normals,
+                const float *const *rgba, int32_t ref, int32_t n_src, const int32_t *srcs, float *out)
+{
+    (void)n;
+    const or_camera *rc = &cams[ref];
+    const int W = rc->width, H = rc->height;
+    int32_t count = 0;
+    for (int r = 0; r < H; ++r) {
+        for (int c = 0; c < W; ++c) {
+            const size_t idx = (size_t)r * W + c;
+            const float ref_depth = depths[ref][idx];
+            if (ref_depth <= 0.0f) continue;                                      /* :1685 */
+            const f3 X = world_point(rc, (float)c, (float)r, ref_depth);
+            const float *rn = &normals[ref][3 * idx];
+            float rcol[4];
+            fuse_colour(rgba[ref], W, H, c, r, rcol);
+            float ps0 = X.x, ps1 = X.y, ps2 = X.z;
+            float ns0 = rn[0], ns1 = rn[1], ns2 = rn[2];
+            float cs0 = rcol[2] * 255.0f, cs1 = rcol[1] * 255.0f, cs2 = rcol[0] * 255.0f;   /* :1705-1709 */
+            int num = 1;
+            for (int j = 0; j < n_src; ++j) {                                    /* :1713-1772 */
+                const int si = srcs[j];
+                if (si < 0) continue;
+                const or_camera *sc = &cams[si];
+                f2 pp;
+                float pd;
+                project(sc, X, &pp, &pd);
+                const int src_c = dm_f2i_sat(pp.x + 0.5f), src_r = dm_f2i_sat(pp.y + 0.5f);
+                if (src_c < 0 || src_c >= sc->width || src_r < 0 || src_r >= sc->height) continue;
+                const size_t sidx = (size_t)src_r * sc->width + src_c;
+                const float sd = depths[si][sidx];
+                if (sd <= 0.0f) continue;
+                const f3 Xs = world_point(sc, (float)src_c, (float)src_r, sd);
+                f2 q;
+                float qd;
+                project(rc, Xs, &q, &qd);
+                const float err = fuse_hypot((float)c - q.x, (float)r - q.y);
+                const float rel = fabsf(pd - sd) / sd;
+                const float *sn = &normals[si][3 * sidx];
+                float dp = dot3(rn[0], rn[1], rn[2], sn[0], sn[1], sn[2]);
+                dp = fmaxf(-1.0f, fminf(1.0f, dp));
+                const float ang = dm_acosf(dp);
+                if (err < 1.0f && rel < 0.01f && ang < 0.149f) {
+                    ps0 += Xs.x; ps1 += Xs.y; ps2 += Xs.z;
+                    ns0 += sn[0]; ns1 += sn[1]; ns2 += sn[2];
+                    float scol[4];
+                    fuse_colour(rgba[si], sc->width, sc->height, src_c, src_r, scol);
+                    cs0 = fmaf(scol[2], 255.0f, cs0);
+                    cs1 = fmaf(scol[1], 255.0f, cs1);
+                    cs2 = fmaf(scol[0], 255.0f, cs2);
+                    ++num;
+                }
+            }
+            if (num >= 3) {                                                       /* :1775-1810 */
+                if (out) {
+                    const float fn = (float)num;
+                    float *o = out + 9 * (size_t)count;
+                    o[0] = ps0 / fn; o[1] = ps1 / fn; o[2] = ps2 / fn;
+                    float a0 = ns0 / fn, a1 = ns1 / fn, a2 = ns2 / fn;
+                    const float len = fuse_hypot(fuse_hypot(a0, a1), a2);
+                    if (len > 0.0f) { a0 /= len; a1 /= len; a2 /= len; }
+                    o[3] = a0; o[4] = a1; o[5] = a2;
+                    o[6] = cs0 / fn; o[7] = cs1 / fn; o[8] = cs2 / fn;
+                }
+                ++count;
+            }
+        }
+    }
+    return count;
+}
+
 void or_detmath_eval(int32_t fn, const float *x, const float *y, float *out, int64_t n)
 {
     for (int64_t i = 0; i < n; ++i) {

@@ -111,6 +111,13 @@ void or_world_point(const or_camera *cam, float x, float y, float depth, float o
 void or_jbu(const float *ref, int32_t W, int32_t H, const float *coarse, int32_t sw, int32_t sh,
             int32_t imagescale, float *out, int32_t nthreads);
 
+/* SimpleFusionKernel (ACMMP.cu:1662-1814) for one reference view + RunFusionCuda's in-order
+ * collection (ACMMP.cu:2064-2071).  cams: n views rescaled to their depth maps; depths[v] (H x W),
+ * normals[v] (3 per pixel), rgba[v] (4 floats per pixel: the reference's colour texture, /255).
+ * out: 9 floats per consistent pixel, pixel order; returns the count (out may be NULL to count). */
+int32_t or_fuse(int32_t n, const or_camera *cams, const float *const *depths, const float *const *normals,
+                const float *const *rgba, int32_t ref, int32_t n_src, const int32_t *srcs, float *out);
+
 /* elementary functions and RNG, exported for tests */
 void or_detmath_eval(int32_t fn, const float *x, const float *y, float *out, int64_t n);
 void or_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

@@ -67,6 +67,8 @@ def lib():
         L.or_world_point.argtypes = [vp, f32, f32, f32, vp]
         L.or_jbu.argtypes = [vp, i32, i32, vp, i32, i32, i32, vp, i32]
         L.or_detmath_eval.argtypes = [i32, vp, vp, vp, C.c_int64]
+        L.or_fuse.argtypes = [i32, vp, vp, vp, vp, i32, i32, vp, vp]
+        L.or_fuse.restype = i32
         L.or_philox.argtypes = [vp, vp, vp]
         L.or_uniform_draw.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
         L.or_uniform_draw.restype = f32
@@ -181,6 +183,26 @@ def jbu(ref, coarse, imagescale: int, nthreads: int = 0):
 
 
 DETMATH_FN = {"exp": 0, "sin": 1, "cos": 2, "asin": 3, "acos": 4, "atan2": 5, "rsqrt": 6, "f2i_sat": 7}
+
+
+def fuse(cams, depths, normals, rgba, ref: int, srcs) -> np.ndarray:
+    """SimpleFusionKernel + in-order collection for one reference view -> (n, 9) float32."""
+    cams = np.frombuffer(np.ascontiguousarray(cams).tobytes(), dtype=CAMERA_DTYPE).copy()
+    d = [np.ascontiguousarray(a, np.float32) for a in depths]
+    nm = [np.ascontiguousarray(a, np.float32) for a in normals]
+    cl = [np.ascontiguousarray(a, np.float32) for a in rgba]
+    n = len(d)
+    pd = (C.c_void_p * n)(*[a.ctypes.data for a in d])
+    pn = (C.c_void_p * n)(*[a.ctypes.data for a in nm])
+    pc = (C.c_void_p * n)(*[a.ctypes.data for a in cl])
+    s = np.ascontiguousarray(srcs, np.int32)
+    L = lib()
+    cnt = L.or_fuse(n, _ptr(cams), C.cast(pd, C.c_void_p), C.cast(pn, C.c_void_p), C.cast(pc, C.c_void_p), ref,
+                    s.size, _ptr(s), None)
+    out = np.zeros((max(cnt, 1), 9), np.float32)
+    L.or_fuse(n, _ptr(cams), C.cast(pd, C.c_void_p), C.cast(pn, C.c_void_p), C.cast(pc, C.c_void_p), ref,
+              s.size, _ptr(s), _ptr(out))
+    return out[:cnt]
 
 
 def detmath(fn: str, x, y=None):

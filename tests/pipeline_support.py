@@ -110,3 +110,24 @@ def final_maps(pipe):
         if a is not None:
             out[(key, v)] = a
     return out
+
+
+class OracleFusion:
+    """capi.Fusion's surface computed by the oracle (tests only)."""
+
+    def __init__(self, cams):
+        self.cams = np.array(cams, copy=True)
+        n = len(self.cams)
+        self.depths, self.normals, self.rgba = [None] * n, [None] * n, [None] * n
+
+    def set_view(self, k, depth, normals, bgr):
+        self.depths[k] = np.ascontiguousarray(depth, np.float32)
+        self.normals[k] = np.ascontiguousarray(normals, np.float32)
+        b = np.asarray(bgr, np.uint8).astype(np.float32)
+        s = np.float32(1.0 / 255.0)
+        rgba = np.stack([b[..., 2] * s, b[..., 1] * s, b[..., 0] * s,
+                         np.full(b.shape[:2], np.float32(255.0) * s, np.float32)], -1)
+        self.rgba[k] = rgba.astype(np.float32)
+
+    def run(self, ref, srcs):
+        return oracle.fuse(self.cams, self.depths, self.normals, self.rgba, ref, srcs)
