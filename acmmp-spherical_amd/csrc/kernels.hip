@@ -1540,6 +1540,32 @@ __global__ void k_filter(const KParams kp, const int colour) {
     if (kp.costs_rm[center] < 0.001f) return;
     const float4* P = kp.planes_rm;
     auto wv = [&](long long i) { return P[i].w; };
+    const int width_ = kp.W, height_ = kp.H;
+    if (py > 4 && py < height_ - 5 && px > 4 && px < width_ - 5) {
+        // interior: all 21 taps exist; the same insertion sort, unrolled over registers (the
+        // early-exit inner loop becomes a "still moving" flag, so NaN orders exactly as :1396)
+        const long long w = width_;
+        float d[21] = {wv(center), wv(center - w), wv(center - 3 * w), wv(center - 5 * w), wv(center + w),
+                       wv(center + 3 * w), wv(center + 5 * w), wv(center - 1), wv(center - 3), wv(center - 5),
+                       wv(center + 1), wv(center + 3), wv(center + 5), wv(center - w + 2), wv(center + w + 2),
+                       wv(center - w - 2), wv(center + w - 2), wv(center - 1 - 2 * w), wv(center + 1 - 2 * w),
+                       wv(center - 1 + 2 * w), wv(center + 1 + 2 * w)};
+#pragma unroll
+        for (int i = 1; i < 21; ++i) {
+            const float tmp = d[i];
+            bool moving = true;
+#pragma unroll
+            for (int j = i; j >= 1; --j) {
+                const bool c = moving && tmp < d[j - 1];
+                const float nd = c ? d[j - 1] : (moving ? tmp : d[j]);
+                moving = c;
+                d[j] = nd;
+            }
+            if (moving) d[0] = tmp;
+        }
+        kp.planes_rm[center].w = d[10];
+        return;
+    }
     float filter[21];
     int index = 0;
     filter[index++] = wv(center);
