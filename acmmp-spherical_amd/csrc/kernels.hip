@@ -1054,6 +1054,12 @@ __device__ __forceinline__ Patch coop_patch_lite(const KParams& kp, bool valid, 
     return pt;
 }
 
+#ifndef ACMMP_REF_PIPE
+#define ACMMP_REF_PIPE true                 // k_eval_ref: every view's texels in flight (two-phase fetch)
+#endif
+#ifndef ACMMP_REF_WAVES
+#define ACMMP_REF_WAVES 1                   // k_eval_ref: minimum waves per SIMD the register budget must allow
+#endif
 constexpr int kRefLanes = 5;                // refinement candidates (ACMMP.cu:870)
 constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 lanes used)
 
@@ -1394,7 +1400,7 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
 
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
 template <int MODEL, int VB, bool GEOM>
-__global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int colour) {
+__global__ __launch_bounds__(256, ACMMP_REF_WAVES) void k_eval_ref(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
@@ -1425,7 +1431,7 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
     float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
     for (int v = 0; v < kp.V; ++v)
         if (!((umask >> v) & 1u)) vcost[v * Pc] = __builtin_nanf("");
-    for_all_views<MODEL, VB, 3, true>(kp, px, py, pt, tp, umask, [&](int v, float c) {
+    for_all_views<MODEL, VB, 3, ACMMP_REF_PIPE>(kp, px, py, pt, tp, umask, [&](int v, float c) {
         vcost[v * Pc] = c;
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
