@@ -981,6 +981,12 @@ __device__ __forceinline__ Patch coop_patch(const KParams& kp, bool valid, int p
 // per sample and ray.y = -sin(lat) once per patch row (it depends on the row only); PINHOLE stores
 // (ray, w) per sample and the texels after them.  32 pixels x 36 samples = 19.2 KB per block for
 // SPHERE (8 blocks per CU).
+// views per NCC chunk in the evaluation kernels (more views than this run as several chunks:
+// the per-sample world point is recomputed per chunk, the accumulators stay in registers)
+#ifndef ACMMP_EVAL_VB
+#define ACMMP_EVAL_VB 4
+#endif
+constexpr int kEvalVB = ACMMP_EVAL_VB;
 #ifndef ACMMP_NB_PIPE
 #define ACMMP_NB_PIPE false                 // experiment switch: all views' texels in flight in k_eval_nb
 #endif
@@ -1064,7 +1070,7 @@ constexpr int kRefLanes = 5;                // refinement candidates (ACMMP.cu:8
 constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 lanes used)
 
 template <int MODEL, int VB>
-__global__ __launch_bounds__(256, 8) void k_eval_nb(const KParams kp, const int colour) {
+__global__ __launch_bounds__(256, MODEL == kSphere ? 8 : 1) void k_eval_nb(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kNbLanes, h = t - lp * kNbLanes;
@@ -1084,7 +1090,7 @@ __global__ __launch_bounds__(256, 8) void k_eval_nb(const KParams kp, const int 
     const float4 ph = plane_at(kp, pos);
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
-    for_all_views<MODEL, VB, 3, ACMMP_NB_PIPE>(kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
+    for_all_views<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, ACMMP_NB_PIPE>(kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
 }
 
 // Joint view selection, aggregation, acceptance and refinement candidates (ACMMP.cu:1146-1311,
@@ -1431,7 +1437,7 @@ __global__ __launch_bounds__(256, ACMMP_REF_WAVES) void k_eval_ref(const KParams
     float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
     for (int v = 0; v < kp.V; ++v)
         if (!((umask >> v) & 1u)) vcost[v * Pc] = __builtin_nanf("");
-    for_all_views<MODEL, VB, 3, ACMMP_REF_PIPE>(kp, px, py, pt, tp, umask, [&](int v, float c) {
+    for_all_views<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, ACMMP_REF_PIPE>(kp, px, py, pt, tp, umask, [&](int v, float c) {
         vcost[v * Pc] = c;
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
