@@ -22,7 +22,7 @@ STATUS = {0: "ok", 1: "invalid argument", 2: "HIP runtime error", 3: "out of dev
 
 # Every symbol include/acmmp.h declares (checked against the header by tests/test_capi_exports.py).
 EXPORTS = [
-    "acmmp_abi_version", "acmmp_create", "acmmp_destroy", "acmmp_status_str", "acmmp_last_error",
+    "acmmp_abi_version", "acmmp_device_count", "acmmp_create", "acmmp_destroy", "acmmp_status_str", "acmmp_last_error",
     "acmmp_set_params", "acmmp_upload_views", "acmmp_upload_depths", "acmmp_set_state",
     "acmmp_set_scaled_state", "acmmp_set_planar_prior", "acmmp_run_patchmatch", "acmmp_run_patchmatch_ex",
     "acmmp_download", "acmmp_download_aux", "acmmp_device_outputs", "acmmp_synchronize", "acmmp_last_timing",
@@ -56,6 +56,7 @@ def load_library(path: str = LIB_PATH):
     L = C.CDLL(path)
     vp, i32, u64 = C.c_void_p, C.c_int, C.c_uint64
     L.acmmp_abi_version.restype = i32
+    L.acmmp_device_count.restype = i32
     L.acmmp_create.argtypes = [i32, C.POINTER(vp)]
     L.acmmp_destroy.argtypes = [vp]
     L.acmmp_destroy.restype = None
@@ -103,7 +104,7 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_planar_prior_host.argtypes = [vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]
     for name in EXPORTS:
         fn = getattr(L, name)
-        if name not in ("acmmp_destroy", "acmmp_status_str", "acmmp_last_error", "acmmp_abi_version",
+        if name not in ("acmmp_destroy", "acmmp_status_str", "acmmp_last_error", "acmmp_abi_version", "acmmp_device_count",
                         "acmmp_depth_from_plane_param", "acmmp_comm_destroy", "acmmp_fusion_last_error",
                         "acmmp_fusion_destroy"):
             fn.restype = i32
@@ -111,6 +112,11 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_fusion_last_error.restype = C.c_char_p
     _lib = L
     return L
+
+
+def device_count() -> int:
+    """Visible HIP devices (the engine's runtime; 0 without a GPU)."""
+    return int(load_library().acmmp_device_count())
 
 
 def _p(a):

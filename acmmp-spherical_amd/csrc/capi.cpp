@@ -135,6 +135,11 @@ extern "C" {
 
 int acmmp_abi_version(void) { return ACMMP_ABI_VERSION; }
 
+int acmmp_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 const char* acmmp_status_str(acmmp_status s) {
     switch (s) {
     case ACMMP_OK: return "ok";

@@ -174,7 +174,9 @@ def main():
     c0 = sc.cameras[0]
     params = types.default_params(num_images=args.n_src + 1, max_iterations=args.iters,
                                   depth_min=float(c0["depth_min"]) * 0.6, depth_max=float(c0["depth_max"]) * 1.2)
-    ctx = capi.Context(local_rank)
+    # one GPU per rank; more ranks than GPUs (rehearsal on a small box) share them round-robin
+    ndev = capi.device_count()
+    ctx = capi.Context(local_rank % ndev if ndev else local_rank)
     ctx.set_params(params)
     ctx.upload_views(sc.images, sc.cameras)
 

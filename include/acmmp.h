@@ -91,6 +91,9 @@ const char *acmmp_status_str(acmmp_status s);
 const char *acmmp_last_error(const acmmp_ctx *ctx);
 int acmmp_abi_version(void);
 
+/* Number of visible HIP devices (0 without a GPU); never fails. */
+int acmmp_device_count(void);
+
 /* The params member + Set{GeomConsistency,Hierarchy,PlanarPrior}Params
  * (ACMMP.cpp:548-565).  Copied; may be called again between runs. */
 acmmp_status acmmp_set_params(acmmp_ctx *ctx, const acmmp_params *params);
