@@ -12,6 +12,8 @@
 // the device side is pinned by injecting prior planes + masks (acmmp_set_planar_prior).
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <thread>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -159,15 +161,20 @@ private:
             if (E.outer >= 0) t_[E.outer].nb[E.outer_slot] = k;
             made.push_back(k);
         }
-        // stitch the fan: triangle with edge starting at vertex a meets the one ending at a
-        for (size_t i = 0; i < made.size(); ++i) first_of_.emplace_back(t_[made[i]].v[0], made[i]);
-        std::sort(first_of_.begin(), first_of_.end());
-        for (int k : made) {
+        // stitch the fan: triangle with edge starting at vertex a meets the one ending at a (the fan
+        // is small -- ~6 triangles -- so a linear search beats sorting)
+        const size_t nm = made.size();
+        for (size_t i = 0; i < nm; ++i) {
+            const int k = made[i];
             const int b = t_[k].v[1];
-            auto it = std::lower_bound(first_of_.begin(), first_of_.end(), std::make_pair(b, -1));
-            const int m = it->second;                    // triangle (b, c, q)
-            t_[k].nb[0] = m;                             // across (b, q)
-            t_[m].nb[1] = k;                             // across (q, b) of m
+            for (size_t j = 0; j < nm; ++j) {
+                const int m = made[j];
+                if (t_[m].v[0] == b) {                   // triangle (b, c, q)
+                    t_[k].nb[0] = m;                     // across (b, q)
+                    t_[m].nb[1] = k;                     // across (q, b) of m
+                    break;
+                }
+            }
         }
         last_ = made.empty() ? -1 : made.back();
     }
@@ -199,6 +206,31 @@ void point_on_ref_cam(int x, int y, float depth, const acmmp_camera& c, float ou
         out[1] = depth * (static_cast<float>(y) - c.K[5]) / c.K[4];
         out[2] = depth;
     }
+}
+
+// Run f(0..n-1) on the host's cores (at most 16 threads); order of completion is irrelevant to
+// every caller (each writes disjoint cells or combines with an order-independent max).
+template <typename F>
+void parallel_for(int n, F&& f) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    const int nt = static_cast<int>(std::min<unsigned>(hw ? hw : 1, 16u));
+    if (nt <= 1 || n < 256) {
+        for (int i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::atomic<int> next(0);
+    auto worker = [&]() {
+        for (;;) {
+            const int b = next.fetch_add(64);
+            if (b >= n) return;
+            const int e = std::min(n, b + 64);
+            for (int i = b; i < e; ++i) f(i);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(worker);
+    worker();
+    for (auto& t : th) t.join();
 }
 
 }  // namespace
@@ -296,19 +328,34 @@ acmmp_status acmmp_planar_prior_host(const acmmp_camera* cam, const float* depth
     acmmp_support_points(costs, W, H, nullptr, 0, &n);
     std::vector<int> xy(2 * static_cast<size_t>(n));
     acmmp_support_points(costs, W, H, xy.data(), n, &n);
-    int m = 0;
-    acmmp_delaunay(xy.data(), n, W, H, nullptr, 0, &m);
-    std::vector<int> tri(6 * static_cast<size_t>(m));
-    acmmp_delaunay(xy.data(), n, W, H, tri.data(), m, &m);
-    // rasterise every triangle inside the image into the label mask (main.cpp:138-165)
-    std::vector<float> mask_tri(P, 0.0f);
-    std::vector<float> plane_params;
+    std::vector<int> tri;
+    if (n > 0) {                                           // triangulate once (ACMMP.cpp:932-955)
+        std::vector<Pt> pts(n);
+        for (int i = 0; i < n; ++i) pts[i] = {xy[2 * i], xy[2 * i + 1]};
+        Delaunay dl(pts, std::max<long long>(std::max(W, H), 1));
+        dl.run();
+        for (const auto& t : dl.triangles())
+            for (int j = 0; j < 3; ++j) { tri.push_back(xy[2 * t[j]]); tri.push_back(xy[2 * t[j] + 1]); }
+    }
+    const int m = static_cast<int>(tri.size() / 6);
+    // triangles inside the image get labels 1, 2, ... in order (main.cpp:138-162)
+    std::vector<uint32_t> label_of(m, 0);
     uint32_t idx = 0;
     for (int k = 0; k < m; ++k) {
         const int* t = &tri[6 * static_cast<size_t>(k)];
         bool inside = true;
         for (int j = 0; j < 3; ++j) inside = inside && t[2 * j] >= 0 && t[2 * j] < W && t[2 * j + 1] >= 0 && t[2 * j + 1] < H;
-        if (!inside) continue;
+        if (inside) label_of[k] = ++idx;
+    }
+    // Rasterise in parallel.  The reference overwrites labels in triangle order, so a pixel ends with
+    // the label of the LAST triangle that covered it -- the largest label: an atomic max gives the same
+    // mask whatever the thread schedule.  Per-triangle planes are independent.
+    std::vector<uint32_t> lab(P, 0u);
+    std::vector<float> plane_params(4 * static_cast<size_t>(idx));
+    parallel_for(m, [&](int k) {
+        const uint32_t label = label_of[k];
+        if (!label) return;
+        const int* t = &tri[6 * static_cast<size_t>(k)];
         const float L01 = static_cast<float>(std::sqrt(std::pow(t[0] - t[2], 2) + std::pow(t[1] - t[3], 2)));
         const float L02 = static_cast<float>(std::sqrt(std::pow(t[0] - t[4], 2) + std::pow(t[1] - t[5], 2)));
         const float L12 = static_cast<float>(std::sqrt(std::pow(t[2] - t[4], 2) + std::pow(t[3] - t[5], 2)));
@@ -318,31 +365,30 @@ acmmp_status acmmp_planar_prior_host(const acmmp_camera* cam, const float* depth
             for (float q = 0; q < 1.0 - p; q += step) {
                 const int x = static_cast<int>(static_cast<double>(p * t[0] + q * t[2]) + (1.0 - p - q) * t[4]);
                 const int y = static_cast<int>(static_cast<double>(p * t[1] + q * t[3]) + (1.0 - p - q) * t[5]);
-                mask_tri[static_cast<size_t>(y) * W + x] = static_cast<float>(idx + 1.0);
+                uint32_t* cell = &lab[static_cast<size_t>(y) * W + x];
+                uint32_t cur = __atomic_load_n(cell, __ATOMIC_RELAXED);
+                while (cur < label && !__atomic_compare_exchange_n(cell, &cur, label, true, __ATOMIC_RELAXED,
+                                                                  __ATOMIC_RELAXED)) {}
             }
         }
-        float n4[4];
-        acmmp_prior_plane_params(cam, depths, W, H, t, n4);
-        plane_params.insert(plane_params.end(), n4, n4 + 4);
-        ++idx;
-    }
-    // prior depth range check (main.cpp:167-180) and CudaPlanarPriorInitialization (ACMMP.cpp:851-861)
-    for (int i = 0; i < W; ++i) {
-        for (int j = 0; j < H; ++j) {
+        acmmp_prior_plane_params(cam, depths, W, H, t, &plane_params[4 * static_cast<size_t>(label - 1)]);
+    });
+    // prior depth range check (main.cpp:167-180) and CudaPlanarPriorInitialization (ACMMP.cpp:851-861);
+    // every pixel is independent (mask_tri holds float labels idx + 1.0, exact below 2^24)
+    parallel_for(H, [&](int j) {
+        for (int i = 0; i < W; ++i) {
             const size_t c = static_cast<size_t>(j) * W + i;
-            if (mask_tri[c] > 0) {
-                const float* pl = &plane_params[4 * (static_cast<size_t>(mask_tri[c]) - 1)];
+            uint32_t l = lab[c];
+            if (l > 0) {
+                const float* pl = &plane_params[4 * static_cast<size_t>(l - 1)];
                 const float d = acmmp_depth_from_plane_param(cam, pl, i, j);
-                if (!(d <= depth_max && d >= depth_min)) mask_tri[c] = 0;
+                if (!(d <= depth_max && d >= depth_min)) l = 0;
             }
+            masks[c] = l;
+            if (l > 0) std::memcpy(prior_planes + 4 * c, &plane_params[4 * static_cast<size_t>(l - 1)], 4 * sizeof(float));
+            else std::memset(prior_planes + 4 * c, 0, 4 * sizeof(float));
         }
-    }
-    for (size_t c = 0; c < P; ++c) {
-        masks[c] = static_cast<uint32_t>(mask_tri[c]);
-        if (mask_tri[c] > 0) std::memcpy(prior_planes + 4 * c, &plane_params[4 * (static_cast<size_t>(mask_tri[c]) - 1)],
-                                         4 * sizeof(float));
-        else std::memset(prior_planes + 4 * c, 0, 4 * sizeof(float));
-    }
+    });
     if (n_triangles) *n_triangles = static_cast<int>(idx);
     return ACMMP_OK;
 }
