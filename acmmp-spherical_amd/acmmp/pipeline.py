@@ -306,6 +306,7 @@ class Pipeline:
         self.log = log or (lambda *a: None)
         self.problems = copy.deepcopy(ds.problems)
         self.pass_index = 0
+        self._scaled = {}                                   # (view, size) -> scaled image, camera
         self.passes = []
         self._pending = []
 
@@ -380,7 +381,10 @@ class Pipeline:
         images, cams = [], []
         for k, vid in enumerate(ids):
             size = prob.cur_image_size if k == 0 else self.problems[vid].cur_image_size
-            img, cam = scale_view(self.ds.images[vid], self.ds.cameras[vid], size)
+            key = (vid, size)
+            if key not in self._scaled:                     # each view is rescaled once per scale
+                self._scaled[key] = scale_view(self.ds.images[vid], self.ds.cameras[vid], size)
+            img, cam = self._scaled[key]
             images.append(img)
             cams.append(cam)
         return ids, images, np.array(cams, dtype=types.CAMERA_DTYPE)
