@@ -142,10 +142,10 @@ ACMMP_HD float det_atan2_special(float y, float x) {
 
 // atan2: branch-free main path for finite non-zero arguments; the rare special arguments are
 // re-evaluated by det_atan2_special in a branch that a wave only takes when one of its lanes needs it.
-ACMMP_HD float det_atan2(float y, float x) {
+// t = min(|x|,|y|) / max(|x|,|y|) computed by the caller (the kernels' projection divides with
+// div_proj, kernels.hip).
+ACMMP_HD float det_atan2_ratio(float y, float x, float t) {
     const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-    const float t = mn / mx;
     const float z = t * t;
     float p = -9.51492460444569588e-04f;
     p = fmaf(p, z, 6.28401106223464012e-03f);
@@ -167,6 +167,11 @@ ACMMP_HD float det_atan2(float y, float x) {
     const bool regular = ay != 0.0f && ax != 0.0f && ax < __builtin_inff() && ay < __builtin_inff();
     if (!regular) r = det_atan2_special(y, x);
     return r;
+}
+
+ACMMP_HD float det_atan2(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    return det_atan2_ratio(y, x, fminf(ax, ay) / fmaxf(ax, ay));
 }
 
 ACMMP_HD float det_rsqrt(float x) { return 1.0f / sqrtf(x); }

@@ -132,6 +132,26 @@ __device__ __forceinline__ float sqrt_proj(float x) {
     return fmaf(-sup, s, x) > 0.0f ? sup : r;
 }
 
+// a / b for the SPHERE projection: LLVM's IEEE f32 division sequence (v_rcp_f32, one Newton step
+// on the reciprocal, two residual corrections, the last one fused) without v_div_scale's exponent
+// pre-scaling and v_div_fixup's special-case pass.  Bit-identical to a / b whenever |b| lies in
+// [2^-125, 2^125] and |a| >= 2^-102 or a == 0 (the sign of a zero quotient may differ); the two
+// projection callers (ty / d and the atan2 ratio min / max) only leave that range for a point
+// closer than 2^-102 to the camera centre (replaced by the principal point) or a quotient below
+// 2^-80, whose contribution to the pixel coordinate is absorbed by cx / cy.
+__device__ __forceinline__ float div_proj(float a, float b) {
+    float y = __builtin_amdgcn_rcpf(b);
+    y = fmaf(fmaf(-b, y, 1.0f), y, y);
+    float q = a * y;
+    q = fmaf(fmaf(-b, q, a), y, q);
+    return fmaf(fmaf(-b, q, a), y, q);
+}
+
+__device__ __forceinline__ float atan2_proj(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    return det_atan2_ratio(y, x, div_proj(fminf(ax, ay), fmaxf(ax, ay)));
+}
+
 // det_asin with its large-argument square root through sqrt_proj: there z = (1 - |x|) / 2 is 0, NaN,
 // negative (|x| > 1 by rounding) or >= 2^-25 (1 - |x| is exact and at least 2^-24), where sqrt_proj
 // equals sqrtf bit for bit.
@@ -158,8 +178,8 @@ __device__ __forceinline__ void project(Cam& c, float3 P, float& ox, float& oy, 
         // point; callers that use the returned depth (fusion) ask for the IEEE square root
         const float d = EXACT_DEPTH ? sqrtf(dot3(tx, ty, tz, tx, ty, tz)) : sqrt_proj(dot3(tx, ty, tz, tx, ty, tz));
         depth = d;
-        const float neg_lat = asin_proj(ty / d);
-        const float lon = det_atan2(tx, tz);
+        const float neg_lat = asin_proj(EXACT_DEPTH ? ty / d : div_proj(ty, d));
+        const float lon = EXACT_DEPTH ? det_atan2(tx, tz) : atan2_proj(tx, tz);
         ox = fmaf(lon * kInv2Pi, c.Wf, c.cx);
         oy = fmaf(neg_lat * kInvPi, c.Hf, c.cy);
         if (d < 1e-6f) { ox = c.cx; oy = c.cy; }        // (:618-622) selected, not branched around
