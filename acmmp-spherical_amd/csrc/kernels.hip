@@ -628,6 +628,31 @@ __device__ __forceinline__ float vw_get(const uint32_t (&vwp)[4], int v) {
     return static_cast<float>((word >> ((v & 7) * 4)) & 15u);
 }
 
+// XCD-aware block order (k_init).  Blocks are dealt round-robin over the 8 XCDs (b and b + 8 share
+// one L2, MI355X_MICROARCH.md "Workgroup dispatch"); launch order gives every XCD every 8th tile of
+// the same rows, so each L2 caches the source-image footprint of all rows in flight.  Instead XCD
+// (b % 8) walks strips x, x + 8, x + 16, ... of ACMMP_XCD_STRIP consecutive logical blocks: its
+// resident blocks cover 1/8 of the rows in flight, and the strips interleave finely enough that every
+// XCD gets the same mix of short-circuited and evaluated rows.  The grid is padded to whole strips
+// per XCD (xcd_grid); surplus blocks find no pixel.  Measured (r01_v23): k_init -10% at 3200x1600
+// V=15 and -16% at 1600x1200 pinhole V=10, neutral at the metric; the same order made k_eval_nb /
+// k_eval_ref 4-9% SLOWER (their lanes of one pixel already share a footprint), so they keep launch order.
+#ifndef ACMMP_XCD_STRIP
+#define ACMMP_XCD_STRIP 256
+#endif
+__device__ __forceinline__ long long xcd_block(unsigned b) {
+    if (ACMMP_XCD_STRIP == 0) return b;
+    const unsigned x = b & 7u, k = b >> 3;
+    const unsigned j = k / ACMMP_XCD_STRIP, r = k - j * ACMMP_XCD_STRIP;
+    return (static_cast<long long>(j) * 8 + x) * ACMMP_XCD_STRIP + r;
+}
+
+static inline unsigned xcd_grid(long long nblocks) {
+    if (ACMMP_XCD_STRIP == 0) return static_cast<unsigned>(nblocks);
+    const long long strips = (nblocks + ACMMP_XCD_STRIP - 1) / ACMMP_XCD_STRIP;
+    return static_cast<unsigned>((strips + 7) / 8 * 8 * ACMMP_XCD_STRIP);
+}
+
 // ------------------------------------------------------------------ kernels: setup
 
 __global__ void k_pad_image(const float* __restrict__ src, size_t pitch, int W, int H, float* __restrict__ dst,
@@ -759,8 +784,11 @@ constexpr int kInitVB = ACMMP_INIT_VB;
 
 template <int MODEL, int VB, int BR, int VMAXB>
 __global__ __launch_bounds__(256) void k_init(const KParams kp) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y * blockDim.y + threadIdx.y;
+    // 16x16 tiles in XCD-aware order (xcd_block) over a row-major grid of ceil(W/16) tiles per row
+    const long long tile = xcd_block(blockIdx.x);
+    const int tiles_x = (kp.W + 15) >> 4;
+    const int x = static_cast<int>(tile % tiles_x) * 16 + threadIdx.x;
+    const int y = static_cast<int>(tile / tiles_x) * 16 + threadIdx.y;
     if (x >= kp.W || y >= kp.H) return;
     const DevCam& rc = kp.cams[0];
     const long long center = static_cast<long long>(y) * kp.W + x;
@@ -1734,7 +1762,7 @@ static inline int pick_vb(int V) { return V <= 1 ? 1 : (V <= 2 ? 2 : (V <= 4 ? 4
     } while (0)
 
 hipError_t launch_init(const KParams& kp, hipStream_t s) {
-    dim3 blk(16, 16), grd(cdiv(kp.W, 16), cdiv(kp.H, 16));
+    dim3 blk(16, 16), grd(xcd_grid(static_cast<long long>(cdiv(kp.W, 16)) * cdiv(kp.H, 16)));
     // branch order of ACMMP.cu:686-793
     const int br = (!kp.geom && !kp.hier) ? kInitRandom : kp.planar ? kInitPlanar : kp.upsample ? kInitUpsample
                                                                                                  : kInitReuse;
