@@ -1144,7 +1144,10 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? 8 : 1) void k_eval_nb(const
 // Joint view selection, aggregation, acceptance and refinement candidates (ACMMP.cu:1146-1311,
 // 797-874).  `iter` selects the view-selection threshold 0.8 exp(-iter^2 / 90) (:1163).
 template <int MODEL, int VB, bool GEOM>
-__global__ __launch_bounds__(256) void k_select(const KParams kp, const int colour, const int iter) {
+#ifndef ACMMP_SEL_WAVES
+#define ACMMP_SEL_WAVES 5                   // k_select: 5 waves per SIMD (96 VGPRs; r01_v24 A/B: 1 -> 5 waves -5%, 6 waves spills)
+#endif
+__global__ __launch_bounds__(256, ACMMP_SEL_WAVES) void k_select(const KParams kp, const int colour, const int iter) {
     const long long q = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
     int px = 0, py = 0;
     if (!colour_pixel(kp, colour, q, px, py)) return;
@@ -1174,6 +1177,20 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
 
     // ---- joint view selection :1146-1208
     constexpr int VMAX = VB < 8 ? VB : kMaxViews;            // pick_vb: V <= VB when VB < 8
+    // up to 4 views the 8 x V cost matrix is read once into registers (all loads in flight together)
+    // and both passes over it below use it; wider launches re-read it from L2
+    constexpr bool kRegCost = VMAX <= 4;
+    float ca[8][kRegCost ? VMAX : 1];
+    if constexpr (kRegCost) {
+#pragma unroll
+        for (int d = 0; d < 8; ++d)
+#pragma unroll
+            for (int v = 0; v < VMAX; ++v) ca[d][v] = v < V ? cost_arr(d, v) : 0.0f;
+    }
+    auto cost_at_dv = [&](int d, int v) -> float {
+        if constexpr (kRegCost) return ca[d][v];
+        else return cost_arr(d, v);
+    };
     // loops over views run to the compile-time VMAX with a guard, so the per-view arrays stay in
     // registers (statically indexed) instead of scratch
     float vsp[VMAX];
@@ -1202,8 +1219,9 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
         float count = 0.0f;
         int count_false = 0;
         float tmpw = 0.0f;
+#pragma unroll
         for (int j = 0; j < 8; j++) {
-            const float c = cost_arr(j, i);
+            const float c = cost_at_dv(j, i);
             if (c < cost_threshold) { tmpw += det_exp(c * c / (-0.18f)); count++; }
             if (c > 1.2f) count_false++;
         }
@@ -1249,16 +1267,23 @@ __global__ __launch_bounds__(256) void k_select(const KParams kp, const int colo
         float fc = 0.0f;
         float4 nb = make_float4(0.f, 0.f, 0.f, 0.f);
         if (GEOM && flag[i]) nb = plane_at(kp, pos[i]);
-        for (int j = 0; j < V; ++j) {
+        auto add_view = [&](int j, float c) {
             const float w = vw_get(vwp, j);
             if (w > 0) {
                 if (GEOM) {
-                    if (flag[i]) fc = fmaf(w, fmaf(0.2f, geom_cost<MODEL>(kp, j + 1, nb, px, py, dc), cost_arr(i, j)), fc);
-                    else fc = fmaf(w, cost_arr(i, j) + 0.1f * 3.0f, fc);
+                    if (flag[i]) fc = fmaf(w, fmaf(0.2f, geom_cost<MODEL>(kp, j + 1, nb, px, py, dc), c), fc);
+                    else fc = fmaf(w, c + 0.1f * 3.0f, fc);
                 } else {
-                    fc = fmaf(w, cost_arr(i, j), fc);
+                    fc = fmaf(w, c, fc);
                 }
             }
+        };
+        if constexpr (kRegCost) {
+#pragma unroll
+            for (int j = 0; j < VMAX; ++j)
+                if (j < V) add_view(j, ca[i][j]);
+        } else {
+            for (int j = 0; j < V; ++j) add_view(j, cost_arr(i, j));
         }
         final_costs[i] = fc / weight_norm;
     }
