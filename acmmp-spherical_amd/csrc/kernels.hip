@@ -156,15 +156,13 @@ __device__ __forceinline__ float atan2_proj(float y, float x) {
 // negative (|x| > 1 by rounding) or >= 2^-25 (1 - |x| is exact and at least 2^-24), where sqrt_proj
 // equals sqrtf bit for bit.
 __device__ __forceinline__ float asin_proj(float x) {
+    // straight-line: one polynomial on selected arguments (no divergent branch, so the compiler can
+    // interleave the views of a chunk; r01_v25 A/B +0.5%)
     const float a = fabsf(x);
-    float r;
-    if (a <= 0.5f) {
-        r = det_asin_core(a, a * a);
-    } else {
-        const float z = (1.0f - a) * 0.5f;
-        r = fmaf(-2.0f, det_asin_core(sqrt_proj(z), z), kPio2Hi) + kPio2Lo;
-    }
-    return copysignf(r, x);
+    const bool small = a <= 0.5f;
+    const float zl = (1.0f - a) * 0.5f;
+    const float c = det_asin_core(small ? a : sqrt_proj(zl), small ? a * a : zl);
+    return copysignf(small ? c : fmaf(-2.0f, c, kPio2Hi) + kPio2Lo, x);
 }
 
 // ProjectonCamera_cu, ACMMP.cu:602-644 (Cam: DevCam in any address space)

@@ -6,8 +6,10 @@ export TMPDIR=/tmp
 TAG=$1; LIBS=$2; shift 2
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
-tail -1 $OUT/pytest.log
+for lib in $LIBS; do
+  ACMMP_LIB=$lib timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest.log 2>&1 || { echo "$lib"; tail -30 $OUT/pytest.log; exit 1; }
+  echo "$(basename $lib): $(tail -1 $OUT/pytest.log)"
+done
 for cfg in "$@"; do
   for lib in $LIBS; do
     ACMMP_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-variant $cfg > $OUT/b.json 2> $OUT/b.err || { tail $OUT/b.err; exit 1; }
