@@ -128,6 +128,9 @@ DevCam acmmp::make_devcam(const acmmp_camera& s) {
     d.C[1] = neg_dot3(s.R[1], s.R[4], s.R[7], s.t[0], s.t[1], s.t[2]);
     d.C[2] = neg_dot3(s.R[2], s.R[5], s.R[8], s.t[0], s.t[1], s.t[2]);
     d.dep_w = 1; d.dep_h = 1;
+    d.Wm1 = s.width - 1; d.Hm1 = s.height - 1;
+    d.Hm1f = static_cast<float>(s.height) - 1.0f;
+    d.pitch4 = 4 * (s.width + 2);
     return d;
 }
 
@@ -268,6 +271,7 @@ acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images,
         DevCam& d = c->dcams[i];
         d = make_devcam(s);
         d.img_off = off[i];
+        d.img_base = c->d_img + off[i];
         d.img_bytes = static_cast<int>(4LL * (s.width + 2) * (s.height + 2));
         d.dep_off = 0; d.dep_w = 1; d.dep_h = 1;
     }

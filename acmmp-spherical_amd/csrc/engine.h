@@ -41,7 +41,10 @@ struct DevCam {
     long long dep_off;              // float offset of the geom depth map (row-major)
     int dep_w, dep_h;
     int img_bytes;                  // bytes of the padded image (buffer descriptor range)
-    int pad_;
+    int Wm1, Hm1;                   // W - 1, H - 1 (texel clamps)
+    float Hm1f;                     // H - 1 as float (SPHERE row clamp)
+    int pitch4;                     // bytes per padded row
+    const float* img_base;          // device address of padded texel (-1,-1) (buffer descriptor base)
 };
 
 // Per-pixel state handed from k_select to k_eval_ref / k_finish (80 bytes).

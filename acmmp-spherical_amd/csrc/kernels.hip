@@ -84,7 +84,8 @@ __device__ __forceinline__ float3 pixel_to_dir(const DevCam& c, int px, int py) 
     return d;
 }
 
-__device__ __forceinline__ float3 rotate_to_world(const DevCam& c, float x, float y, float z) {
+template <typename Cam>
+__device__ __forceinline__ float3 rotate_to_world(Cam& c, float x, float y, float z) {
     float3 r;
     r.x = dot3(c.R[0], c.R[3], c.R[6], x, y, z) + c.C[0];
     r.y = dot3(c.R[1], c.R[4], c.R[7], x, y, z) + c.C[1];
@@ -109,14 +110,50 @@ __device__ __forceinline__ float3 world_point(const DevCam& c, float x, float y,
 
 // The same at an integer reference pixel whose ray `d` is already known (SPHERE's
 // camera-frame point is ray * depth exactly as Get3DPointonWorld_cu rounds it).
-template <int MODEL>
-__device__ __forceinline__ float3 world_point_ray(const DevCam& c, int x, int y, float depth, float4 d) {
+template <int MODEL, typename Cam>
+__device__ __forceinline__ float3 world_point_ray(Cam& c, int x, int y, float depth, float4 d) {
     if (MODEL == kSphere) {
         return rotate_to_world(c, d.x * depth, d.y * depth, d.z * depth);
     } else {
         return rotate_to_world(c, (depth * (static_cast<float>(x) - c.K[2])) * c.inv_fx,
                                (depth * (static_cast<float>(y) - c.K[5])) * c.inv_fy, depth);
     }
+}
+
+// Single-instruction helpers with the hardware's own semantics (inline asm, so the compiler neither
+// canonicalises operands nor widens them): v_cvt_i32_f32 truncates, saturates and maps NaN to 0
+// (= f2i_sat); v_med3_i32 clamps; v_mad_u32_u24 multiplies 24-bit operands; v_max/min_f32 return
+// the non-NaN operand of a quiet NaN (= fmaxf / fminf on the values these kernels produce, which
+// are never signalling NaNs).
+__device__ __forceinline__ int cvt_i32(float x) {
+    int r;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ int clamp_m1(int x, int hi) {          // clampi(x, -1, hi), hi wave-uniform
+    int r;
+    asm("v_med3_i32 %0, %1, -1, %2" : "=v"(r) : "v"(x), "s"(hi));
+    return r;
+}
+__device__ __forceinline__ unsigned mad_u24(unsigned a, unsigned b, unsigned c) {  // a, b < 2^24, b uniform
+    unsigned r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float max_abs(float a, float b) {
+    float r;
+    asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float min_abs(float a, float b) {
+    float r;
+    asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float clamp0(float x, float hi) {        // fminf(fmaxf(x, 0), hi), hi uniform
+    float r;
+    asm("v_max_f32_e32 %0, 0, %1\n\tv_min_f32_e32 %0, %2, %0" : "=&v"(r) : "v"(x), "s"(hi));
+    return r;
 }
 
 // sqrtf for the SPHERE projection: LLVM's IEEE f32 sqrt lowering (v_sqrt_f32, then the +-1 ulp
@@ -148,8 +185,7 @@ __device__ __forceinline__ float div_proj(float a, float b) {
 }
 
 __device__ __forceinline__ float atan2_proj(float y, float x) {
-    const float ax = fabsf(x), ay = fabsf(y);
-    return det_atan2_ratio(y, x, div_proj(fminf(ax, ay), fmaxf(ax, ay)));
+    return det_atan2_ratio(y, x, div_proj(min_abs(x, y), max_abs(x, y)));
 }
 
 // det_asin with its large-argument square root through sqrt_proj: there z = (1 - |x|) / 2 is 0, NaN,
@@ -288,24 +324,25 @@ struct Tap {
     f32x2 top, bot;
 };
 
-template <bool Y_IN_RANGE>
-__device__ __forceinline__ Tap fetch_tap(__amdgpu_buffer_rsrc_t rs, int pitch, int W, int H, float x, float y) {
+// ix = clampi(f2i_sat(floor x), -1, W-1), iy likewise (SPHERE: y already in [0, H-1], so iy = (int)floor y
+// >= 0); the footprint's top-left texel sits at byte (iy+1)*pitch4 + (ix+1)*4 of the padded image.
+// SPHERE moves the +1 row into the scalar offsets (top row soffset = pitch4, bottom = 2*pitch4).
+template <bool Y_IN_RANGE, typename Cam>
+__device__ __forceinline__ Tap fetch_tap(__amdgpu_buffer_rsrc_t rs, Cam& c, float x, float y) {
     const float fx = floorf(x), fy = floorf(y);
     Tap t;
     t.a = x - fx;
     t.b = y - fy;
-    int ix = static_cast<int>(fminf(fmaxf(fx, -1.0f), static_cast<float>(W - 1)));
-    ix = fx != fx ? 0 : ix;
-    int iy;
+    const unsigned ix4 = (static_cast<unsigned>(clamp_m1(cvt_i32(fx), c.Wm1)) << 2) + 4u;
     if (Y_IN_RANGE) {
-        iy = static_cast<int>(fy);
+        const unsigned off = mad_u24(static_cast<unsigned>(cvt_i32(fy)), c.pitch4, ix4);
+        t.top = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, c.pitch4, 0));
+        t.bot = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 2 * c.pitch4, 0));
     } else {
-        iy = static_cast<int>(fminf(fmaxf(fy, -1.0f), static_cast<float>(H - 1)));
-        iy = fy != fy ? 0 : iy;
+        const unsigned off = mad_u24(static_cast<unsigned>(clamp_m1(cvt_i32(fy), c.Hm1) + 1), c.pitch4, ix4);
+        t.top = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+        t.bot = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, c.pitch4, 0));
     }
-    const int off = (__mul24(iy + 1, pitch) + ix + 1) * 4;
-    t.top = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
-    t.bot = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, pitch * 4, 0));
     return t;
 }
 
@@ -375,6 +412,14 @@ __device__ __forceinline__ Patch make_patch(const KParams& kp, int px, int py) {
 // STAGED: 0 = samples recomputed here, 1 = (ray, w) + texel staged in LDS, 2 = (w, texel) staged
 // and the ray re-read from the ray tables (less LDS per pixel, more blocks per CU), 3 = the
 // k_eval_nb layout of coop_patch_nb.
+#ifndef ACMMP_PIPEG
+#define ACMMP_PIPEG 1                       // views per texel-fetch group when the caller does not pipeline
+#endif
+constexpr int kPipeG = ACMMP_PIPEG;
+#ifndef ACMMP_RC_CONST_PIPE
+#define ACMMP_RC_CONST_PIPE 0               // 1: PIPE callers (k_eval_ref) also read the reference camera per sample (A/B r01_v27: -3%)
+#endif
+
 template <int MODEL, int VB, int STAGED, bool PIPE>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv, float (&cost)[VB]) {
@@ -411,6 +456,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
         }
     }
     const int R = kp.R, inc = kp.inc;
+    constexpr int G = PIPE ? VB : kPipeG;
     int s = 0;
     for (int i = -R; i <= R; i += inc) {
         for (int j = -R; j <= R; j += inc, ++s) {
@@ -437,7 +483,13 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 rw = patch_sample<MODEL>(kp, px, py, s, i, j, pt.center, r);
             }
             const float w = rw.w;
-            const float3 P = world_point_ray<MODEL>(rc, px + i, py + j, depth_from_plane(ph, rw), rw);
+            // reference camera through the constant address space too: scalar loads per sample
+            // instead of 12 wave-uniform VGPRs held across the loop
+            float3 P;
+            if (!PIPE || ACMMP_RC_CONST_PIPE)
+                P = world_point_ray<MODEL>(ccams[0], px + i, py + j, depth_from_plane(ph, rw), rw);
+            else
+                P = world_point_ray<MODEL>(rc, px + i, py + j, depth_from_plane(ph, rw), rw);
             const float wr = w * r;
             Tap tap[VB];
             bool ok[VB];
@@ -467,22 +519,22 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                     ok[v] = true;
                     if (MODEL == kSphere) {
                         sx = fmaf(-floorf(sx * c.invW), c.Wf, sx);
-                        sy = fminf(fmaxf(sy, 0.0f), c.Hf - 1.0f);
+                        sy = clamp0(sy, c.Hm1f);
                     } else {
                         ok[v] = !(sx < 0.0f || sx >= c.Wf || sy < 0.0f || sy >= c.Hf);
                     }
                     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                        const_cast<float*>(kp.img + c.img_off), 0, c.img_bytes, 0x00020000);
-                    tap[v] = fetch_tap<MODEL == kSphere>(rs, c.img_pitch, c.W, c.H, sx, sy);
-                    if (!PIPE) ACMMP_ACCUMULATE(v);
+                        const_cast<float*>(c.img_base), 0, c.img_bytes, 0x00020000);
+                    tap[v] = fetch_tap<MODEL == kSphere>(rs, c, sx, sy);
+                    if (G == 1) ACMMP_ACCUMULATE(v);
                 }
-            }
-            // PIPE: every view's texels are in flight before the first is used (more latency
-            // hidden per wave, ~6 more VGPRs per view)
-            if (PIPE) {
+                // G > 1: views are consumed in groups of G, a group's texels all in flight before the
+                // first is used (PIPE: the whole chunk; ~6 VGPRs per view in flight)
+                if (G > 1 && ((v + 1) % G == 0 || v == VB - 1)) {
 #pragma unroll
-                for (int v = 0; v < VB; ++v)
-                    if (v < nv) ACMMP_ACCUMULATE(v);
+                    for (int u = v - (v % G); u <= v; ++u)
+                        if (u < nv) ACMMP_ACCUMULATE(u);
+                }
             }
 #undef ACMMP_ACCUMULATE
         }
@@ -1112,6 +1164,9 @@ __device__ __forceinline__ Patch coop_patch_lite(const KParams& kp, bool valid, 
 #ifndef ACMMP_REF_WAVES
 #define ACMMP_REF_WAVES 1                   // k_eval_ref: minimum waves per SIMD the register budget must allow
 #endif
+#ifndef ACMMP_REF_WAVES_SPH
+#define ACMMP_REF_WAVES_SPH ACMMP_REF_WAVES // the same for the SPHERE non-geom instance (80 VGPRs at 6 waves, no spills)
+#endif
 constexpr int kRefLanes = 5;                // refinement candidates (ACMMP.cu:870)
 constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 lanes used)
 
@@ -1477,7 +1532,7 @@ __global__ __launch_bounds__(256, ACMMP_SEL_WAVES) void k_select(const KParams k
 
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
 template <int MODEL, int VB, bool GEOM>
-__global__ __launch_bounds__(256, ACMMP_REF_WAVES) void k_eval_ref(const KParams kp, const int colour) {
+__global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_SPH : ACMMP_REF_WAVES) void k_eval_ref(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
