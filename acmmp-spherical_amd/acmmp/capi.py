@@ -26,7 +26,7 @@ EXPORTS = [
     "acmmp_set_params", "acmmp_upload_views", "acmmp_upload_depths", "acmmp_set_state",
     "acmmp_set_scaled_state", "acmmp_set_planar_prior", "acmmp_run_patchmatch", "acmmp_run_patchmatch_ex",
     "acmmp_download", "acmmp_download_aux", "acmmp_device_outputs", "acmmp_synchronize", "acmmp_last_timing",
-    "acmmp_last_kernel_timing", "acmmp_last_work", "acmmp_jbu",
+    "acmmp_last_kernel_timing", "acmmp_last_work", "acmmp_texel_bytes", "acmmp_jbu",
     "acmmp_debug_ncc", "acmmp_debug_geom",
     "acmmp_support_points", "acmmp_delaunay", "acmmp_prior_plane_params", "acmmp_depth_from_plane_param",
     "acmmp_planar_prior_host",
@@ -78,6 +78,7 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_last_timing.argtypes = [vp, vp]
     L.acmmp_last_kernel_timing.argtypes = [vp, vp, vp]
     L.acmmp_last_work.argtypes = [vp, vp, vp]
+    L.acmmp_texel_bytes.argtypes = [vp]
     L.acmmp_synchronize.argtypes = [vp]
     L.acmmp_jbu.argtypes = [vp, vp, i32, i32, vp, i32, i32, i32, vp]
     L.acmmp_debug_ncc.argtypes = [vp, i32, vp, vp, vp, vp]
@@ -251,6 +252,10 @@ class Context:
         e, t = C.c_ulonglong(0), C.c_ulonglong(0)
         self._check(self.L.acmmp_last_work(self.h, C.byref(e), C.byref(t)), "last_work")
         return e.value, t.value
+
+    def texel_bytes(self) -> int:
+        """Bytes per source texel the NCC fetches read (2: binary16 copy, 4: fp32, 0: no views)."""
+        return int(self.L.acmmp_texel_bytes(self.h))
 
     def jbu(self, ref, coarse, imagescale: int):
         ref = np.ascontiguousarray(ref, np.float32)

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -36,6 +37,7 @@ struct acmmp_ctx {
     std::vector<DevCam> dcams;
     DevCam* d_cams = nullptr;
     float* d_img = nullptr;
+    uint16_t* d_img16 = nullptr;     // binary16 copy of d_img (null when some texel is not exact)
 
     float* d_dep = nullptr;
     bool has_depths = false;
@@ -189,7 +191,7 @@ void acmmp_destroy(acmmp_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    dfree(c->d_cams); dfree(c->d_img); dfree(c->d_dep); dfree(c->d_dirs);
+    dfree(c->d_cams); dfree(c->d_img); dfree(c->d_img16); dfree(c->d_dep); dfree(c->d_dirs);
     dfree(c->d_sph_row); dfree(c->d_sph_col); dfree(c->d_spatial);
     dfree(c->d_planes_rm); dfree(c->d_costs_rm); dfree(c->d_pre); dfree(c->d_sel_rm);
     dfree(c->d_scaled); dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_scratch); dfree(c->d_work);
@@ -247,6 +249,7 @@ acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images,
         total = (total + 63) & ~63LL;
     }
     HIP_TRY(c, dalloc(c->d_img, static_cast<size_t>(total)));
+    HIP_TRY(c, hipMemsetAsync(c->d_img, 0, sizeof(float) * static_cast<size_t>(total), c->stream));  // gaps between views
     float* staging = nullptr;
     size_t staging_cap = 0;
     for (int i = 0; i < n; ++i) {
@@ -265,6 +268,25 @@ acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images,
     }
     dfree(staging);
 
+    // binary16 copy for the NCC fetches when it holds the same values (8-bit images always do):
+    // half the bytes per footprint, so twice the views fit a cache level.
+    // ACMMP_TEX16=0 in the environment keeps the fp32 fetches (A/B switch; identical results).
+    dfree(c->d_img16);
+    const char* tex16_env = std::getenv("ACMMP_TEX16");
+    if (!(tex16_env && tex16_env[0] == '0')) {
+        int* d_flag = nullptr;
+        HIP_TRY(c, dalloc(c->d_img16, static_cast<size_t>(total)));
+        HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&d_flag), sizeof(int)));
+        int inexact = 0;
+        hipError_t e = hipMemsetAsync(d_flag, 0, sizeof(int), c->stream);
+        if (e == hipSuccess) e = launch_to_f16(c->d_img, total, c->d_img16, d_flag, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(&inexact, d_flag, sizeof(int), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        dfree(d_flag);
+        HIP_TRY(c, e);
+        if (inexact) dfree(c->d_img16);
+    }
+
     c->dcams.assign(n, DevCam{});
     for (int i = 0; i < n; ++i) {
         const acmmp_camera& s = cams[i];
@@ -273,6 +295,9 @@ acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images,
         d.img_off = off[i];
         d.img_base = c->d_img + off[i];
         d.img_bytes = static_cast<int>(4LL * (s.width + 2) * (s.height + 2));
+        d.img16_base = c->d_img16 ? c->d_img16 + off[i] : nullptr;
+        d.img16_bytes = static_cast<int>(2LL * (s.width + 2) * (s.height + 2));
+        d.pitch2 = 2 * (s.width + 2);
         d.dep_off = 0; d.dep_w = 1; d.dep_h = 1;
     }
     HIP_TRY(c, dalloc(c->d_cams, static_cast<size_t>(n)));
@@ -457,6 +482,7 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     }
     kp.cams = c->d_cams;
     kp.img = c->d_img;
+    kp.tex16 = c->d_img16 != nullptr;
     kp.dep = c->d_dep;
     kp.dirs = c->d_dirs;
     kp.sph_row = c->d_sph_row;
@@ -595,6 +621,11 @@ acmmp_status acmmp_last_work(const acmmp_ctx* c, unsigned long long* evaluated, 
     *evaluated = c->work_busy;
     *total = c->work_total;
     return ACMMP_OK;
+}
+
+int acmmp_texel_bytes(const acmmp_ctx* c) {
+    if (!c || !c->d_img) return 0;
+    return c->d_img16 ? 2 : 4;
 }
 
 acmmp_status acmmp_last_kernel_timing(const acmmp_ctx* c, float ms[4], int launches[4]) {

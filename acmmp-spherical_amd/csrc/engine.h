@@ -45,6 +45,11 @@ struct DevCam {
     float Hm1f;                     // H - 1 as float (SPHERE row clamp)
     int pitch4;                     // bytes per padded row
     const float* img_base;          // device address of padded texel (-1,-1) (buffer descriptor base)
+    // binary16 copy of the padded image (same layout, 2 B per texel), present when every texel of
+    // every view is exactly representable (8-bit images are): half the cache footprint, same values
+    const uint16_t* img16_base;
+    int img16_bytes;
+    int pitch2;                     // bytes per padded binary16 row
 };
 
 // Per-pixel state handed from k_select to k_eval_ref / k_finish (80 bytes).
@@ -61,6 +66,7 @@ struct PixState {
 
 struct KParams {
     int model;                      // kPinhole / kSphere, uniform over all views
+    int tex16;                      // 1: NCC fetches read the binary16 images (DevCam::img16_base)
     int W, H, Wh, N, V;             // ref size, colour row width ceil(W/2), images, source views
     int R, inc, nside, S;           // patch radius, radius_increment, offsets per axis, samples
     int rows;                       // rows the reference's checkerboard grid covers
@@ -142,6 +148,9 @@ hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int s
                       float* out, hipStream_t s);
 hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,
                         float* out, hipStream_t s);
+// Padded fp32 images -> binary16 copy; *inexact (device int, pre-zeroed) is set when a texel is not
+// exactly representable as a normal binary16 number or zero.
+hipError_t launch_to_f16(const float* src, long long n, uint16_t* dst, int* inexact, hipStream_t s);
 hipError_t launch_pad_image(const float* src, size_t pitch_floats, int W, int H, float* dst, int dst_pitch,
                             hipStream_t s);
 

@@ -327,12 +327,32 @@ struct Tap {
 // ix = clampi(f2i_sat(floor x), -1, W-1), iy likewise (SPHERE: y already in [0, H-1], so iy = (int)floor y
 // >= 0); the footprint's top-left texel sits at byte (iy+1)*pitch4 + (ix+1)*4 of the padded image.
 // SPHERE moves the +1 row into the scalar offsets (top row soffset = pitch4, bottom = 2*pitch4).
-template <bool Y_IN_RANGE, typename Cam>
+//
+// TEX = 1 reads the binary16 copy instead (DevCam::img16_base, same padded layout, 2 B per texel):
+// each row of the footprint is one 4-byte load at a 2-byte-aligned offset (the driver runs gfx9 in
+// unaligned-access mode) holding (t(ix), t(ix+1)) as (lo, hi) halves, kept raw in top.x / bot.x.
+template <int TEX, bool Y_IN_RANGE, typename Cam>
 __device__ __forceinline__ Tap fetch_tap(__amdgpu_buffer_rsrc_t rs, Cam& c, float x, float y) {
     const float fx = floorf(x), fy = floorf(y);
     Tap t;
     t.a = x - fx;
     t.b = y - fy;
+    if (TEX == 1) {
+        const unsigned ix2 = (static_cast<unsigned>(clamp_m1(cvt_i32(fx), c.Wm1)) << 1) + 2u;
+        unsigned top, bot;
+        if (Y_IN_RANGE) {
+            const unsigned off = mad_u24(static_cast<unsigned>(cvt_i32(fy)), c.pitch2, ix2);
+            top = __builtin_amdgcn_raw_buffer_load_b32(rs, off, c.pitch2, 0);
+            bot = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 2 * c.pitch2, 0);
+        } else {
+            const unsigned off = mad_u24(static_cast<unsigned>(clamp_m1(cvt_i32(fy), c.Hm1) + 1), c.pitch2, ix2);
+            top = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+            bot = __builtin_amdgcn_raw_buffer_load_b32(rs, off, c.pitch2, 0);
+        }
+        t.top.x = __builtin_bit_cast(float, top);
+        t.bot.x = __builtin_bit_cast(float, bot);
+        return t;
+    }
     const unsigned ix4 = (static_cast<unsigned>(clamp_m1(cvt_i32(fx), c.Wm1)) << 2) + 4u;
     if (Y_IN_RANGE) {
         const unsigned off = mad_u24(static_cast<unsigned>(cvt_i32(fy)), c.pitch4, ix4);
@@ -346,7 +366,28 @@ __device__ __forceinline__ Tap fetch_tap(__amdgpu_buffer_rsrc_t rs, Cam& c, floa
     return t;
 }
 
+// binary16 row pair v = (lo, hi): hi - lo rounded once to binary32 (v_fma_mix_f32 hi * 1 + (-lo)),
+// the same bits as the fp32 subtraction of the two converted texels (conversion is exact)
+__device__ __forceinline__ float f16_pair_diff(unsigned v) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, 1.0, -%1 op_sel:[1,0,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(v));
+    return r;
+}
+// fmaf(a, d, (float)lo(v)) in one v_fma_mix_f32
+__device__ __forceinline__ float f16_fma_lo(float a, float d, unsigned v) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,0,1]" : "=v"(r) : "v"(a), "v"(d), "v"(v));
+    return r;
+}
+
+template <int TEX = 0>
 __device__ __forceinline__ float lerp_tap(const Tap& t) {
+    if (TEX == 1) {
+        const unsigned top = __builtin_bit_cast(unsigned, t.top.x), bot = __builtin_bit_cast(unsigned, t.bot.x);
+        const float r0 = f16_fma_lo(t.a, f16_pair_diff(top), top);
+        const float r1 = f16_fma_lo(t.a, f16_pair_diff(bot), bot);
+        return fmaf(t.b, r1 - r0, r0);
+    }
     const float r0 = fmaf(t.a, t.top.y - t.top.x, t.top.x);
     const float r1 = fmaf(t.a, t.bot.y - t.bot.x, t.bot.x);
     return fmaf(t.b, r1 - r0, r0);
@@ -420,7 +461,7 @@ constexpr int kPipeG = ACMMP_PIPEG;
 #define ACMMP_RC_CONST_PIPE 0               // 1: PIPE callers (k_eval_ref) also read the reference camera per sample (A/B r01_v27: -3%)
 #endif
 
-template <int MODEL, int VB, int STAGED, bool PIPE>
+template <int MODEL, int VB, int STAGED, bool PIPE, int TEX>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv, float (&cost)[VB]) {
     // SPHERE: the weight sum of every view is the pixel's patch sum (hypothesis- and view-independent);
@@ -496,7 +537,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             // accumulate view v's sample (ACMMP.cu:488-498)
 #define ACMMP_ACCUMULATE(v)                                                  \
             do {                                                             \
-                const float sp = lerp_tap(tap[v]);                           \
+                const float sp = lerp_tap<TEX>(tap[v]);                      \
                 if (ok[v]) {                                                 \
                     if (MODEL == kPinhole) {                                 \
                         sbw[v] += w;                                         \
@@ -523,9 +564,10 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                     } else {
                         ok[v] = !(sx < 0.0f || sx >= c.Wf || sy < 0.0f || sy >= c.Hf);
                     }
-                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                        const_cast<float*>(c.img_base), 0, c.img_bytes, 0x00020000);
-                    tap[v] = fetch_tap<MODEL == kSphere>(rs, c, sx, sy);
+                    const __amdgpu_buffer_rsrc_t rs = TEX == 1
+                        ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000)
+                        : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(c.img_base), 0, c.img_bytes, 0x00020000);
+                    tap[v] = fetch_tap<TEX, MODEL == kSphere>(rs, c, sx, sy);
                     if (G == 1) ACMMP_ACCUMULATE(v);
                 }
                 // G > 1: views are consumed in groups of G, a group's texels all in flight before the
@@ -643,9 +685,9 @@ __device__ __forceinline__ float4 perturbed_normal(float4 v, float4 n, Rng& rs, 
 // ------------------------------------------------------------------ cost-vector helpers
 
 // Evaluate all source views of plane `ph` and hand each cost to f(view0, cost) in view order.
-template <int MODEL, int VB, int STAGED, bool PIPE, typename F>
-__device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
-                                              uint32_t wave_mask, F&& f) {
+template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, typename F>
+__device__ __forceinline__ void for_all_views_t(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
+                                                uint32_t wave_mask, F&& f) {
     int v = 0;
     const int V = kp.V;
     while (true) {
@@ -665,12 +707,20 @@ __device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py,
         }
         if (nv == 0) break;
         float cost[VB];
-        ncc_chunk<MODEL, VB, STAGED, PIPE>(kp, px, py, pt, ph, vlist, nv, cost);
+        ncc_chunk<MODEL, VB, STAGED, PIPE, TEX>(kp, px, py, pt, ph, vlist, nv, cost);
 #pragma unroll
         for (int k = 0; k < VB; ++k)
             if (k < nv) f(vlist[k] - 1, cost[k]);
         if (v >= V) break;
     }
+}
+
+// The same over the binary16 images when the context has them (launch-uniform branch).
+template <int MODEL, int VB, int STAGED, bool PIPE, typename F>
+__device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
+                                              uint32_t wave_mask, F&& f) {
+    if (kp.tex16) for_all_views_t<MODEL, VB, STAGED, PIPE, 1>(kp, px, py, pt, ph, wave_mask, f);
+    else for_all_views_t<MODEL, VB, STAGED, PIPE, 0>(kp, px, py, pt, ph, wave_mask, f);
 }
 
 __device__ __forceinline__ float vw_get(const uint32_t (&vwp)[4], int v) {
@@ -704,6 +754,18 @@ static inline unsigned xcd_grid(long long nblocks) {
 }
 
 // ------------------------------------------------------------------ kernels: setup
+
+__global__ void k_to_f16(const float* __restrict__ src, long long n, uint16_t* __restrict__ dst,
+                         int* __restrict__ inexact) {
+    const long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = src[i];
+    const _Float16 h = static_cast<_Float16>(x);
+    const float back = static_cast<float>(h);
+    // exact, finite, and zero or normal binary16 (no subnormal inputs to v_fma_mix_f32)
+    if (!(back == x) || (x != 0.0f && !(fabsf(x) >= 6.103515625e-05f)) || fabsf(x) > 65504.0f) atomicOr(inexact, 1);
+    dst[i] = __builtin_bit_cast(uint16_t, h);
+}
 
 __global__ void k_pad_image(const float* __restrict__ src, size_t pitch, int W, int H, float* __restrict__ dst,
                             int dpitch) {
@@ -1170,8 +1232,11 @@ __device__ __forceinline__ Patch coop_patch_lite(const KParams& kp, bool valid, 
 constexpr int kRefLanes = 5;                // refinement candidates (ACMMP.cu:870)
 constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 lanes used)
 
+#ifndef ACMMP_NB_WAVES
+#define ACMMP_NB_WAVES 8                    // k_eval_nb (SPHERE): minimum waves per SIMD the register budget must allow
+#endif
 template <int MODEL, int VB>
-__global__ __launch_bounds__(256, MODEL == kSphere ? 8 : 1) void k_eval_nb(const KParams kp, const int colour) {
+__global__ __launch_bounds__(256, MODEL == kSphere ? ACMMP_NB_WAVES : 1) void k_eval_nb(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kNbLanes, h = t - lp * kNbLanes;
@@ -1793,6 +1858,12 @@ __global__ void k_debug(const KParams kp, int which, int n, const int* __restric
 // ------------------------------------------------------------------ host launchers
 
 static inline int cdiv(long long a, int b) { return static_cast<int>((a + b - 1) / b); }
+
+hipError_t launch_to_f16(const float* src, long long n, uint16_t* dst, int* inexact, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    k_to_f16<<<static_cast<unsigned>((n + 255) / 256), 256, 0, s>>>(src, n, dst, inexact);
+    return hipGetLastError();
+}
 
 hipError_t launch_pad_image(const float* src, size_t pitch_floats, int W, int H, float* dst, int dst_pitch,
                             hipStream_t s) {

@@ -169,6 +169,12 @@ acmmp_status acmmp_last_kernel_timing(const acmmp_ctx *ctx, float ms[4], int lau
  * (ACMMP.cu:501-503) and are short-circuited; the roofline counts only evaluated pixels. */
 acmmp_status acmmp_last_work(const acmmp_ctx *ctx, unsigned long long *evaluated, unsigned long long *total);
 
+/* Bytes per source texel the NCC fetches read: 2 when every texel of the uploaded views is exactly
+ * a binary16 number (8-bit images are) and the engine keeps a binary16 copy of them, 4 for the fp32
+ * images, 0 before acmmp_upload_views.  Results are identical either way; the
+ * environment variable ACMMP_TEX16=0 at upload time forces 4.  No reference counterpart. */
+int acmmp_texel_bytes(const acmmp_ctx *ctx);
+
 /* ---- device buffers and the multi-GPU communicator (no reference counterpart:
  * the reference is single-GPU and exchanges depth maps through dmb files) ------------------- */
 

@@ -62,10 +62,10 @@ SCENES = [
 ]
 
 
-def make(kind, W, H, V, seed=0):
+def make(kind, W, H, V, seed=0, quantize=True):
     if kind == "pinhole":
-        return scene.pinhole_scene(W, H, n_src=V, seed=seed)
-    return scene.sphere_scene(W, H, n_src=V, seed=seed)
+        return scene.pinhole_scene(W, H, n_src=V, seed=seed, quantize=quantize)
+    return scene.sphere_scene(W, H, n_src=V, seed=seed, quantize=quantize)
 
 
 @pytest.mark.parametrize("kind,W,H,V", SCENES, ids=[f"{k}-{w}x{h}-v{v}" for k, w, h, v in SCENES])
@@ -75,6 +75,39 @@ def test_full_run_bitexact(ctx, oracle_mod, kind, W, H, V):
     g = gpu_run(ctx, sc, p, seed=4321)
     o = oracle_mod.run_patchmatch(oracle_mod.Problem(sc.images, sc.cameras, p), seed=4321)
     check(g, o)
+
+
+@pytest.mark.parametrize("kind", ["pinhole", "sphere"])
+@pytest.mark.parametrize("fmt", ["f16", "fp32-forced", "fp32-unquantized"])
+def test_texel_formats_bitexact(ctx, oracle_mod, monkeypatch, kind, fmt):
+    """8-bit images are fetched from the binary16 copy, others (and ACMMP_TEX16=0) from fp32:
+    both equal the oracle bit for bit."""
+    sc = make(kind, 88, 52, 3, seed=23, quantize=(fmt != "fp32-unquantized"))
+    if fmt == "fp32-forced":
+        monkeypatch.setenv("ACMMP_TEX16", "0")
+    p = params_for(sc)
+    g = gpu_run(ctx, sc, p, seed=99)
+    assert ctx.texel_bytes() == (2 if fmt == "f16" else 4)
+    o = oracle_mod.run_patchmatch(oracle_mod.Problem(sc.images, sc.cameras, p), seed=99)
+    check(g, o)
+    monkeypatch.delenv("ACMMP_TEX16", raising=False)
+    ctx.upload_views(sc.images, sc.cameras)                    # back to the default format
+
+
+def test_texel_bytes_state(oracle_mod):
+    with capi.Context(0) as c:
+        assert c.texel_bytes() == 0
+        sc = make("sphere", 64, 32, 1, seed=3)
+        c.set_params(params_for(sc))
+        c.upload_views(sc.images, sc.cameras)
+        assert c.texel_bytes() == 2
+        imgs = [im.copy() for im in sc.images]
+        imgs[1][5, 7] = 70000.0                                # beyond binary16's range
+        c.upload_views(imgs, sc.cameras)
+        assert c.texel_bytes() == 4
+        imgs[1][5, 7] = 2.0 ** -20                              # exact binary16 subnormal
+        c.upload_views(imgs, sc.cameras)
+        assert c.texel_bytes() == 4
 
 
 @pytest.mark.parametrize("kind", ["pinhole", "sphere"])
