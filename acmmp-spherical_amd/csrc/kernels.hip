@@ -457,6 +457,10 @@ __device__ __forceinline__ Patch make_patch(const KParams& kp, int px, int py) {
 #define ACMMP_PIPEG 1                       // views per texel-fetch group when the caller does not pipeline
 #endif
 constexpr int kPipeG = ACMMP_PIPEG;
+#ifndef ACMMP_PIPEG16
+#define ACMMP_PIPEG16 ACMMP_PIPEG            // the same for the binary16 fetches (half the tap registers)
+#endif
+constexpr int kPipeG16 = ACMMP_PIPEG16;
 #ifndef ACMMP_RC_CONST_PIPE
 #define ACMMP_RC_CONST_PIPE 0               // 1: PIPE callers (k_eval_ref) also read the reference camera per sample (A/B r01_v27: -3%)
 #endif
@@ -497,7 +501,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
         }
     }
     const int R = kp.R, inc = kp.inc;
-    constexpr int G = PIPE ? VB : kPipeG;
+    constexpr int G = PIPE ? VB : (TEX == 1 ? kPipeG16 : kPipeG);
     int s = 0;
     for (int i = -R; i <= R; i += inc) {
         for (int j = -R; j <= R; j += inc, ++s) {
