@@ -504,7 +504,8 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     constexpr int G = PIPE ? VB : (TEX == 1 ? kPipeG16 : kPipeG);
     int s = 0;
     for (int i = -R; i <= R; i += inc) {
-        for (int j = -R; j <= R; j += inc, ++s) {
+        int jj = 0;                                      // s % nside without a division per sample
+        for (int j = -R; j <= R; j += inc, ++s, ++jj) {
             float r;
             float4 rw;
             if (STAGED == 1) {
@@ -513,7 +514,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             } else if (STAGED == 3) {                    // coop_patch_nb layout
                 const float4 q = pt.rw[s];
                 if (MODEL == kSphere) {
-                    rw = make_float4(q.x, pt.rr[s % kp.nside], q.y, q.z);
+                    rw = make_float4(q.x, pt.rr[jj], q.y, q.z);
                     r = q.w;
                 } else {
                     rw = q;

@@ -147,6 +147,13 @@ def test_ncc_and_geom_kernels_bitexact(ctx, oracle_mod, kind):
     nrm = rng.normal(size=(n, 3))
     nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
     planes = np.concatenate([nrm, rng.uniform(-1, 8, (n, 1))], 1).astype(np.float32)
+    # extreme plane offsets: zero, tiny and (pinhole) huge |w| through the ray-plane division
+    planes[::37, 3] = 0.0
+    planes[5::37, 3] = 3e-25
+    if kind == "pinhole":
+        # (SPHERE projections beyond |t| ~ 1.8e19, where |t|^2 overflows, are outside the documented
+        # range of the projection's division -- such depths never arise from [dmin, dmax])
+        planes[11::37, 3] = -2e20
     depths = [np.abs(rng.normal(5, 1, im.shape)).astype(np.float32) for im in sc.images]
     depths[1][::7, ::5] = 0.0                                    # src_depth == 0 -> 3 (ACMMP.cu:658)
     ctx.set_params(p)
