@@ -23,9 +23,11 @@ seed + 7919 * pass + 31 * ref_image_id + run.
 """
 from __future__ import annotations
 
+import contextlib
 import copy
 import math
 import os
+import time
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -309,6 +311,15 @@ class Pipeline:
         self._scaled = {}                                   # (view, size) -> scaled image, camera
         self.passes = []
         self._pending = []
+        self.stage_s = {}                                   # host wall seconds per stage (profiling)
+
+    @contextlib.contextmanager
+    def _timed(self, stage):
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            self.stage_s[stage] = self.stage_s.get(stage, 0.0) + time.perf_counter() - t0
 
     # -- sharding
     def owner(self, i: int) -> int:
@@ -393,7 +404,8 @@ class Pipeline:
     def process_problem(self, idx, geom, planar, hier, multi):
         prob = self.problems[idx]
         ref = prob.ref_image_id
-        ids, images, cams = self._inputs(idx)
+        with self._timed("inputs"):
+            ids, images, cams = self._inputs(idx)
         c0 = cams[0]
         p = types.default_params(num_images=len(images), depth_min=float(c0["depth_min"]) * 0.6,
                                  depth_max=float(c0["depth_max"]) * 1.2)
@@ -407,6 +419,39 @@ class Pipeline:
             p["hierarchy"] = 1
         e = self.engine
         H, W = images[0].shape
+        with self._timed("upload"):
+            self._upload(e, p, images, cams, ids, ref, geom, hier, H, W)
+        run_seed = self.seed + 7919 * self.pass_index + 31 * ref
+        with self._timed("patchmatch"):
+            e.run_patchmatch(run_seed)
+            planes, costs = e.download()
+        if planar:                                                   # main.cpp:113-187
+            p["planar_prior"] = 1
+            with self._timed("planar_prior_host"):
+                prior, masks, _ = capi.planar_prior_host(c0, planes[..., 3], costs, float(p["depth_min"]),
+                                                         float(p["depth_max"]))
+            with self._timed("upload"):
+                e.set_params(p)
+                e.set_planar_prior(prior, masks)
+            with self._timed("patchmatch"):
+                e.run_patchmatch(run_seed + 1)
+                planes, costs = e.download()
+        with self._timed("store"):
+            key = "depths_geom" if geom else "depths"
+            self._save(key, ref, planes[..., 3].copy(), e if isinstance(e, capi.Context) else None)
+            self.store.put("normals", ref, planes[..., :3].copy())
+            self.store.put("costs", ref, costs)
+            if self.out_folder:
+                d = os.path.join(self.out_folder, "ACMMP", f"2333_{ref:08d}")
+                os.makedirs(d, exist_ok=True)
+                io.write_dmb(os.path.join(d, key + ".dmb"), planes[..., 3])
+                io.write_dmb(os.path.join(d, "normals.dmb"), planes[..., :3])
+                io.write_dmb(os.path.join(d, "costs.dmb"), costs)
+        return planes, costs
+
+    def _upload(self, e, p, images, cams, ids, ref, geom, hier, H, W):
+        """InuputInitialization + the state reloads of ProcessProblem (ACMMP.cpp:567-679, 772-843)."""
+        multi = bool(p["multi_geometry"])
         if geom:
             key = "depths_geom" if multi else "depths"
             e.set_params(p)
@@ -442,28 +487,6 @@ class Pipeline:
         else:
             e.set_params(p)
             e.upload_views(images, cams)
-        run_seed = self.seed + 7919 * self.pass_index + 31 * ref
-        e.run_patchmatch(run_seed)
-        planes, costs = e.download()
-        if planar:                                                   # main.cpp:113-187
-            p["planar_prior"] = 1
-            prior, masks, _ = capi.planar_prior_host(c0, planes[..., 3], costs, float(p["depth_min"]),
-                                                     float(p["depth_max"]))
-            e.set_params(p)
-            e.set_planar_prior(prior, masks)
-            e.run_patchmatch(run_seed + 1)
-            planes, costs = e.download()
-        key = "depths_geom" if geom else "depths"
-        self._save(key, ref, planes[..., 3].copy(), e if isinstance(e, capi.Context) else None)
-        self.store.put("normals", ref, planes[..., :3].copy())
-        self.store.put("costs", ref, costs)
-        if self.out_folder:
-            d = os.path.join(self.out_folder, "ACMMP", f"2333_{ref:08d}")
-            os.makedirs(d, exist_ok=True)
-            io.write_dmb(os.path.join(d, key + ".dmb"), planes[..., 3])
-            io.write_dmb(os.path.join(d, "normals.dmb"), planes[..., :3])
-            io.write_dmb(os.path.join(d, "costs.dmb"), costs)
-        return planes, costs
 
     # -- RunFusionCuda (ACMMP.cu:1817-2105), after the last pass
     def run_fusion(self, fusion_factory=None, ply_path: str | None = None):
@@ -514,7 +537,8 @@ class Pipeline:
         imagescale = max(scaled.shape[0] // coarse.shape[0], scaled.shape[1] // coarse.shape[1])
         if imagescale == 1:                                          # ACMMP.cpp:1076-1079
             return None
-        out = self.engine.jbu(scaled, coarse, imagescale)
+        with self._timed("jbu"):
+            out = self.engine.jbu(scaled, coarse, imagescale)
         self.store.put("depths", ref, out)
         if self.out_folder:
             d = os.path.join(self.out_folder, "ACMMP", f"2333_{ref:08d}")

@@ -49,6 +49,8 @@ def main():
     acc = scene.depth_accuracy(d0, sc.gt_depth) if d0.shape == sc.gt_depth.shape else None
     print(json.dumps({"views": a.views, "size": [a.width, a.height], "passes": [p.name for p in pipe.passes],
                       "total_s": round(total, 3), "s_per_view_pass": round(total / (a.views * len(pipe.passes)), 4),
+                      "pass_s": [round(t, 3) for _, t in times[1:]] + [round(time.perf_counter() - last[0], 3)],
+                      "stages_s": {k: round(v, 3) for k, v in sorted(pipe.stage_s.items())},
                       "ref_view_frac_within_1pct_gt": acc}), flush=True)
 
 
