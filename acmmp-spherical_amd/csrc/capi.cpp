@@ -414,6 +414,18 @@ static unsigned long long colour_pixels(const acmmp_ctx* c, const KParams& kp, i
     return n;
 }
 
+// Split point of the refinement evaluation: about half the views, a multiple of the
+// 4-view NCC chunk above 4 views; 0 (no split) for one view, for colour grids too large for the
+// 32-bit queue entries, or with ACMMP_REF_SPLIT=0 in the environment (A/B switch).
+static int ref_split_point(int V, size_t Pc) {
+    static const int enabled = [] {
+        const char* e = std::getenv("ACMMP_REF_SPLIT");
+        return e ? std::atoi(e) : 1;
+    }();
+    if (!enabled || V < 2 || Pc >= (static_cast<size_t>(1) << 29)) return 0;
+    return V <= 4 ? V / 2 : 4 * std::max(1, (V / 2 + 2) / 4);
+}
+
 static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     const acmmp_params& p = c->params;
     if (!c->has_params) return fail(c, ACMMP_ERR_STATE, "set_params first");
@@ -466,19 +478,19 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     HIP_TRY(c, dalloc(c->d_spatial, static_cast<size_t>(c->model == kSphere ? c->H : 1) * kp.S));
     HIP_TRY(c, launch_spatial_table(kp, c->d_spatial, c->stream));
     // half-sweep scratch slab: carve the pieces of engine.h's KParams out of one allocation
-    size_t off[10];
+    size_t off[12];
     {
         const size_t VP = static_cast<size_t>(kp.V) * Pc;
-        const size_t sizes[9] = {sizeof(float) * 8 * VP, sizeof(int) * 8 * Pc,
-                                 sizeof(float4) * 5 * Pc, sizeof(float) * 5 * Pc, sizeof(float) * 5 * Pc,
-                                 sizeof(PixState) * Pc, sizeof(float) * VP, sizeof(float) * VP,
-                                 sizeof(float) * 5 * VP};
+        const size_t sizes[11] = {sizeof(float) * 8 * VP, sizeof(int) * 8 * Pc,
+                                  sizeof(float4) * 5 * Pc, sizeof(float) * 5 * Pc, sizeof(float) * 5 * Pc,
+                                  sizeof(PixState) * Pc, sizeof(float) * VP, sizeof(float) * VP,
+                                  sizeof(float) * 5 * VP, sizeof(uint32_t) * 5 * Pc, sizeof(unsigned)};
         off[0] = 0;
-        for (int k = 0; k < 9; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
+        for (int k = 0; k < 11; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
     }
-    if (c->scratch_bytes < off[9]) {
-        HIP_TRY(c, dalloc(c->d_scratch, off[9]));
-        c->scratch_bytes = off[9];
+    if (c->scratch_bytes < off[11]) {
+        HIP_TRY(c, dalloc(c->d_scratch, off[11]));
+        c->scratch_bytes = off[11];
     }
     kp.cams = c->d_cams;
     kp.img = c->d_img;
@@ -505,6 +517,9 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.cvec[0] = reinterpret_cast<float*>(c->d_scratch + off[6]);
     kp.cvec[1] = reinterpret_cast<float*>(c->d_scratch + off[7]);
     kp.cand_vcost = reinterpret_cast<float*>(c->d_scratch + off[8]);
+    kp.surv = reinterpret_cast<uint32_t*>(c->d_scratch + off[9]);
+    kp.surv_count = reinterpret_cast<unsigned*>(c->d_scratch + off[10]);
+    kp.ref_split = ref_split_point(kp.V, Pc);
     if (!c->d_work) HIP_TRY(c, dalloc(c->d_work, 256));
     kp.work = c->d_work;
     return ACMMP_OK;

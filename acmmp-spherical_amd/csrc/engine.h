@@ -108,6 +108,12 @@ struct KParams {
     PixState* pst;                  // [Pc]
     unsigned long long* work;       // [256] k_eval_nb pixels with NCC work (SPHERE patch sum >= 1e-6), per block % 256
     long long Pc;                   // H * Wh
+    // split refinement: k_eval_ref evaluates views [0, ref_split) of every candidate,
+    // drops the ones whose partial aggregate already cannot beat cost_now, and queues the rest
+    // (ci * 8 + candidate) for k_eval_ref_tail, which adds views [ref_split, V).  0 = no split.
+    int ref_split;
+    uint32_t* surv;                 // [5 * Pc] queued candidates
+    unsigned* surv_count;           // queue length (zeroed before each k_eval_ref)
 };
 
 // Per-half-sweep output buffers of the colour being updated.

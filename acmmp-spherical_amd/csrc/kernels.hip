@@ -1630,10 +1630,15 @@ __global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_
     for (int v = 0; v < kp.V; ++v) if (vw_get(vwp, v) > 0.0f) mask |= 1u << v;
     float temp_cost = 0.0f;
     const uint32_t umask = wave_or(mask, kp.V);
+    // split: this kernel takes views [0, S) only, unless the whole wave sits in the SPHERE degenerate
+    // band (every cost 2.0 without a sample: nothing to save)
+    const int S = kp.ref_split;
+    const bool split = S > 0 && __any(!(MODEL == kSphere && pt.sbw < 1e-6f));
+    const uint32_t amask = split ? (umask & ((1u << S) - 1u)) : umask;
     float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
     for (int v = 0; v < kp.V; ++v)
-        if (!((umask >> v) & 1u)) vcost[v * Pc] = __builtin_nanf("");
-    for_all_views<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, ACMMP_REF_PIPE>(kp, px, py, pt, tp, umask, [&](int v, float c) {
+        if (!((amask >> v) & 1u)) vcost[v * Pc] = __builtin_nanf("");
+    for_all_views<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, ACMMP_REF_PIPE>(kp, px, py, pt, tp, amask, [&](int v, float c) {
         vcost[v * Pc] = c;
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
@@ -1641,7 +1646,64 @@ __global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_
             else temp_cost = fmaf(w, c, temp_cost);
         }
     });
-    kp.cand_cost[h * Pc + ci] = temp_cost / weight_norm;
+    const float partial = temp_cost / weight_norm;
+    if (!split) { kp.cand_cost[h * Pc + ci] = partial; return; }
+    // Every remaining term w * (c [+ 0.1 geom]) is >= 0 (c in [0, 2], geom in [0, 3]), so the fma chain
+    // only grows and, divided by weight_norm > 0, the final cost is >= `partial`: when
+    // !(partial < cost_now) the candidate cannot pass k_finish's `temp_cost < cost_now` (cost_now
+    // only decreases there), and `partial` stands in for its cost.  Prior-restricted pixels accept by
+    // restricted cost instead and always finish.  A survivor that selected no view >= S still goes to
+    // the tail: the views >= S its wave evaluates complete its cost vector, which the current-plane
+    // cost cache takes over if it wins (a NaN entry there costs k_select a divergent re-evaluation).
+    const PixState& st = kp.pst[ci];
+    const bool done = !(st.flags & 1u) && !(partial < st.cost_now);
+    kp.cand_cost[h * Pc + ci] = done ? partial : temp_cost;
+    const unsigned long long b = __ballot(!done);
+    if (b) {                                                 // queue the wave's survivors
+        const int lane = __lane_id();
+        const int leader = __ffsll(static_cast<long long>(b)) - 1;
+        unsigned base = 0u;
+        if (lane == leader) base = atomicAdd(kp.surv_count, static_cast<unsigned>(__popcll(b)));
+        base = __shfl(base, leader);
+        if (!done) kp.surv[base + __popcll(b & ((1ull << lane) - 1ull))] = static_cast<uint32_t>(ci * 8 + h);
+    }
+}
+
+// The queued candidates' views [ref_split, V) (one lane per candidate, patch samples recomputed),
+// continuing the aggregate's fma chain in view order from k_eval_ref's partial sum.
+template <int MODEL, int VB, bool GEOM>
+__global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const int colour) {
+    const unsigned n = *kp.surv_count;
+    const long long Pc = kp.Pc;
+    const int S = kp.ref_split;
+    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint32_t rec = kp.surv[i];
+        const long long ci = rec >> 3;
+        const int h = static_cast<int>(rec & 7u);
+        const int py = static_cast<int>(ci / kp.Wh);
+        const int px = 2 * static_cast<int>(ci - static_cast<long long>(py) * kp.Wh) + ((py + colour) & 1);
+        const PixState& st = kp.pst[ci];
+        const uint4 vw = st.vw;
+        const float weight_norm = st.weight_norm;
+        const uint32_t vwp[4] = {vw.x, vw.y, vw.z, vw.w};
+        uint32_t mask = 0u;
+        for (int v = S; v < kp.V; ++v) if (vw_get(vwp, v) > 0.0f) mask |= 1u << v;
+        const uint32_t umask = wave_or(mask, kp.V);
+        const float4 dc = ray_at<MODEL>(kp, px, py);
+        const float4 tp = kp.cand[h * Pc + ci];
+        const Patch pt = make_patch<MODEL>(kp, px, py);
+        float temp_cost = kp.cand_cost[h * Pc + ci];
+        float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
+        for_all_views<MODEL, (VB > kEvalVB ? kEvalVB : VB), 0, ACMMP_REF_PIPE>(kp, px, py, pt, tp, umask, [&](int v, float c) {
+            vcost[v * Pc] = c;
+            const float w = vw_get(vwp, v);
+            if (w > 0.0f) {
+                if (GEOM) temp_cost = fmaf(w, fmaf(0.1f, geom_cost<MODEL>(kp, v + 1, tp, px, py, dc), c), temp_cost);
+                else temp_cost = fmaf(w, c, temp_cost);
+            }
+        });
+        kp.cand_cost[h * Pc + ci] = temp_cost / weight_norm;
+    }
 }
 
 // Refinement acceptance in candidate order (ACMMP.cu:902-935), hierarchy gate (:1315-1324), store.
@@ -1941,8 +2003,15 @@ hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut ou
     if (kp.geom) ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, true><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
     else ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, false><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
     ACMMP_MARK(2);
+    if (kp.ref_split > 0 && (e = hipMemsetAsync(kp.surv_count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
     if (kp.geom) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, true><<<cdiv(npix, kRefPix), 256, lds_ref, s>>>(kp, colour)));
     else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, false><<<cdiv(npix, kRefPix), 256, lds_ref, s>>>(kp, colour)));
+    if (kp.ref_split > 0) {
+        // grid-stride over the queue (its length is known on the device only): at most 5 per pixel
+        const unsigned grd = static_cast<unsigned>(std::min<long long>(cdiv(5 * npix, 256), 8192));
+        if (kp.geom) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, true><<<grd, 256, 0, s>>>(kp, colour)));
+        else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, false><<<grd, 256, 0, s>>>(kp, colour)));
+    }
     ACMMP_MARK(3);
     if (kp.model == kSphere) k_finish<kSphere><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, out);
     else k_finish<kPinhole><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, out);

@@ -3,7 +3,7 @@
 # Usage: bash scripts/ab_bench.sh TAG "LIB1 LIB2 ..." ["bench args"]
 set -o pipefail
 export TMPDIR=/tmp
-TAG=$1; LIBS=$2; ARGS=${3:-"--no-cpu-baseline --no-variant"}
+TAG=$1; LIBS=$2; ARGS=${3:-"--no-cpu-baseline --no-variant --no-pipeline"}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }

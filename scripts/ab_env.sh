@@ -11,7 +11,7 @@ tail -1 $OUT/pytest.log
 for cfg in "$@"; do
   for rep in 1 2; do
     for e in $ENVS; do
-      env $e timeout -k 10 300 python bench.py --no-cpu-baseline --no-variant $cfg > $OUT/b.json 2> $OUT/b.err || { tail $OUT/b.err; exit 1; }
+      env $e timeout -k 10 300 python bench.py --no-cpu-baseline --no-variant --no-pipeline $cfg > $OUT/b.json 2> $OUT/b.err || { tail $OUT/b.err; exit 1; }
       python -c "import json;d=json.load(open('$OUT/b.json'));print('$e', '$cfg', d['value'], d['ms_per_depth_map'], d['stages_ms']['init'], d['roofline']['half_sweep_kernels_ms'])"
     done
   done
