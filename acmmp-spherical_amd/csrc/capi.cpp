@@ -422,7 +422,12 @@ static int ref_split_point(int V, size_t Pc) {
         const char* e = std::getenv("ACMMP_REF_SPLIT");
         return e ? std::atoi(e) : 1;
     }();
+    static const int at = [] {                              // ACMMP_REF_SPLIT_AT=S: fixed split (A/B)
+        const char* e = std::getenv("ACMMP_REF_SPLIT_AT");
+        return e ? std::atoi(e) : 0;
+    }();
     if (!enabled || V < 2 || Pc >= (static_cast<size_t>(1) << 29)) return 0;
+    if (at > 0) return at < V ? at : 0;
     return V <= 4 ? V / 2 : 4 * std::max(1, (V / 2 + 2) / 4);
 }
 
