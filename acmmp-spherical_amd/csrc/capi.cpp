@@ -483,19 +483,20 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     HIP_TRY(c, dalloc(c->d_spatial, static_cast<size_t>(c->model == kSphere ? c->H : 1) * kp.S));
     HIP_TRY(c, launch_spatial_table(kp, c->d_spatial, c->stream));
     // half-sweep scratch slab: carve the pieces of engine.h's KParams out of one allocation
-    size_t off[12];
+    size_t off[13];
     {
         const size_t VP = static_cast<size_t>(kp.V) * Pc;
-        const size_t sizes[11] = {sizeof(float) * 8 * VP, sizeof(int) * 8 * Pc,
+        const size_t sizes[12] = {sizeof(float) * 8 * VP, sizeof(int) * 8 * Pc,
                                   sizeof(float4) * 5 * Pc, sizeof(float) * 5 * Pc, sizeof(float) * 5 * Pc,
                                   sizeof(PixState) * Pc, sizeof(float) * VP, sizeof(float) * VP,
-                                  sizeof(float) * 5 * VP, sizeof(uint32_t) * 5 * Pc, sizeof(unsigned)};
+                                  sizeof(float) * 5 * VP, sizeof(uint32_t) * 5 * Pc, sizeof(unsigned),
+                                  sizeof(float4) * Pc};
         off[0] = 0;
-        for (int k = 0; k < 11; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
+        for (int k = 0; k < 12; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
     }
-    if (c->scratch_bytes < off[11]) {
-        HIP_TRY(c, dalloc(c->d_scratch, off[11]));
-        c->scratch_bytes = off[11];
+    if (c->scratch_bytes < off[12]) {
+        HIP_TRY(c, dalloc(c->d_scratch, off[12]));
+        c->scratch_bytes = off[12];
     }
     kp.cams = c->d_cams;
     kp.img = c->d_img;
@@ -524,6 +525,7 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.cand_vcost = reinterpret_cast<float*>(c->d_scratch + off[8]);
     kp.surv = reinterpret_cast<uint32_t*>(c->d_scratch + off[9]);
     kp.surv_count = reinterpret_cast<unsigned*>(c->d_scratch + off[10]);
+    kp.psum = reinterpret_cast<float4*>(c->d_scratch + off[11]);
     kp.ref_split = ref_split_point(kp.V, Pc);
     if (!c->d_work) HIP_TRY(c, dalloc(c->d_work, 256));
     kp.work = c->d_work;

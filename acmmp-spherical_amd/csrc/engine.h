@@ -114,6 +114,7 @@ struct KParams {
     int ref_split;
     uint32_t* surv;                 // [5 * Pc] queued candidates
     unsigned* surv_count;           // queue length (zeroed before each k_eval_ref)
+    float4* psum;                   // [Pc] (patch sum w, sum w r, sum w r^2, centre texel) for the tail
 };
 
 // Per-half-sweep output buffers of the colour being updated.

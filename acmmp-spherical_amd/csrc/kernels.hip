@@ -1621,6 +1621,11 @@ __global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_
     }
     const Patch pt = coop_patch_nb<MODEL, kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
     if (!valid) return;
+    if (kp.ref_split > 0 && h == 0) {                        // the tail's patch, without re-summing it
+        const DevCam& rc = kp.cams[0];
+        kp.psum[ci] = make_float4(pt.sbw, pt.sref, pt.srr,
+                                  texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py));
+    }
     const float4 dc = ray_at<MODEL>(kp, px, py);
     const float4 tp = kp.cand[h * Pc + ci];
     const float depth_before = depth_from_plane(tp, dc);
@@ -1691,7 +1696,10 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
         const uint32_t umask = wave_or(mask, kp.V);
         const float4 dc = ray_at<MODEL>(kp, px, py);
         const float4 tp = kp.cand[h * Pc + ci];
-        const Patch pt = make_patch<MODEL>(kp, px, py);
+        Patch pt;                                            // make_patch's values, from k_eval_ref
+        const float4 ps = kp.psum[ci];
+        pt.rw = nullptr; pt.rr = nullptr; pt.wr = nullptr; pt.stride = 0;
+        pt.sbw = ps.x; pt.sref = ps.y; pt.srr = ps.z; pt.center = ps.w;
         float temp_cost = kp.cand_cost[h * Pc + ci];
         float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
         for_all_views<MODEL, (VB > kEvalVB ? kEvalVB : VB), 0, ACMMP_REF_PIPE>(kp, px, py, pt, tp, umask, [&](int v, float c) {
