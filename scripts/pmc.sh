@@ -5,7 +5,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc}
-ARGS=${2:-"--steps 1 --warmup 0 --no-cpu-baseline"}
+ARGS=${2:-"--steps 1 --warmup 0 --no-cpu-baseline --no-variant --no-pipeline"}
 mkdir -p $OUT
 i=0
 for CTRS in "FETCH_SIZE" "WRITE_SIZE" \

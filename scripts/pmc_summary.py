@@ -13,7 +13,7 @@ import json
 import re
 from collections import defaultdict
 
-SHORT = ("k_eval_nb", "k_select", "k_eval_ref", "k_finish", "k_init", "k_merge", "k_filter", "k_pad_image",
+SHORT = ("k_eval_nb", "k_select", "k_eval_ref", "k_eval_ref_tail", "k_pick", "k_finish", "k_init", "k_merge", "k_filter", "k_pad_image",
          "k_ray_tables", "k_spatial", "k_jbu")
 
 
