@@ -233,30 +233,44 @@ void parallel_for(int n, F&& f) {
     for (auto& t : th) t.join();
 }
 
+// GetSupportPoints (ACMMP.cpp:904-929): per 5x5 block in column-major block order, the first
+// minimum-cost pixel of the block scanned column by column (strict '>' keeps the first), kept when
+// its cost is < 0.1.  Column strips run in parallel into their own lists, concatenated in strip
+// order -- the reference's point order, which the Delaunay insertion order depends on.
+std::vector<int> support_points(const float* costs, int W, int H) {
+    const int step = 5;
+    const int strips = (W + step - 1) / step;
+    std::vector<std::vector<int>> per(strips);
+    parallel_for(strips, [&](int s) {
+        const int col = s * step;
+        const int cb = std::min(W, col + step);
+        std::vector<int>& out = per[s];
+        for (int row = 0; row < H; row += step) {
+            float min_cost = 2.0f;
+            int tx = 0, ty = 0;
+            const int rb = std::min(H, row + step);
+            for (int c = col; c < cb; ++c)
+                for (int r = row; r < rb; ++r) {
+                    const float v = costs[static_cast<size_t>(r) * W + c];
+                    if (v < 2.0f && min_cost > v) { tx = c; ty = r; min_cost = v; }
+                }
+            if (min_cost < 0.1f) { out.push_back(tx); out.push_back(ty); }
+        }
+    });
+    std::vector<int> all;
+    for (const auto& v : per) all.insert(all.end(), v.begin(), v.end());
+    return all;
+}
+
 }  // namespace
 
 extern "C" {
 
 acmmp_status acmmp_support_points(const float* costs, int W, int H, int* xy, int cap, int* n_out) {
     if (!costs || !n_out || W <= 0 || H <= 0 || cap < 0 || (cap > 0 && !xy)) return ACMMP_ERR_INVALID_ARGUMENT;
-    const int step = 5;
-    int n = 0;
-    for (int col = 0; col < W; col += step) {
-        for (int row = 0; row < H; row += step) {
-            float min_cost = 2.0f;
-            int tx = 0, ty = 0;
-            const int cb = std::min(W, col + step), rb = std::min(H, row + step);
-            for (int c = col; c < cb; ++c)
-                for (int r = row; r < rb; ++r) {
-                    const float v = costs[static_cast<size_t>(r) * W + c];
-                    if (v < 2.0f && min_cost > v) { tx = c; ty = r; min_cost = v; }
-                }
-            if (min_cost < 0.1f) {
-                if (n < cap) { xy[2 * n] = tx; xy[2 * n + 1] = ty; }
-                ++n;
-            }
-        }
-    }
+    const std::vector<int> pts = support_points(costs, W, H);
+    const int n = static_cast<int>(pts.size() / 2);
+    if (xy && cap > 0) std::memcpy(xy, pts.data(), sizeof(int) * 2 * static_cast<size_t>(std::min(n, cap)));
     *n_out = n;
     return n <= cap ? ACMMP_OK : ACMMP_ERR_INVALID_ARGUMENT;
 }
@@ -324,10 +338,8 @@ acmmp_status acmmp_planar_prior_host(const acmmp_camera* cam, const float* depth
     if (!cam || !depths || !costs || !prior_planes || !masks || W <= 0 || H <= 0) return ACMMP_ERR_INVALID_ARGUMENT;
     const size_t P = static_cast<size_t>(W) * H;
     // GetSupportPoints + DelaunayTriangulation (main.cpp:120-121)
-    int n = 0;
-    acmmp_support_points(costs, W, H, nullptr, 0, &n);
-    std::vector<int> xy(2 * static_cast<size_t>(n));
-    acmmp_support_points(costs, W, H, xy.data(), n, &n);
+    const std::vector<int> xy = support_points(costs, W, H);
+    const int n = static_cast<int>(xy.size() / 2);
     std::vector<int> tri;
     if (n > 0) {                                           // triangulate once (ACMMP.cpp:932-955)
         std::vector<Pt> pts(n);
