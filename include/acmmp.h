@@ -161,7 +161,9 @@ acmmp_status acmmp_last_timing(const acmmp_ctx *ctx, float ms[3]);
 
 /* Per-kernel device time of the last run's half-sweeps (HIP events around every launch, on the
  * kernels' stream): summed ms and launch count for [k_eval_nb, k_select, k_eval_ref, k_finish]
- * (the four kernels one CheckerboardPropagation half-sweep is split into). */
+ * (the stages one CheckerboardPropagation half-sweep is split into).  The k_eval_ref
+ * bucket includes its tail launch (k_eval_ref_tail); the neighbour pick (k_pick) runs before the
+ * k_eval_nb bucket opens and is in the propagation stage time only. */
 acmmp_status acmmp_last_kernel_timing(const acmmp_ctx *ctx, float ms[4], int launches[4]);
 
 /* Work accounting of the last run's k_eval_nb launches: pixels whose NCCs were evaluated, and all
