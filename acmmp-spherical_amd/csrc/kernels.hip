@@ -1234,6 +1234,12 @@ __device__ __forceinline__ Patch coop_patch_lite(const KParams& kp, bool valid, 
 #ifndef ACMMP_REF_WAVES_SPH
 #define ACMMP_REF_WAVES_SPH ACMMP_REF_WAVES // the same for the SPHERE non-geom instance (80 VGPRs at 6 waves, no spills)
 #endif
+#ifndef ACMMP_REF_LITE
+#define ACMMP_REF_LITE 0                    // k_eval_ref: 1 = (w, texel) staging, rays re-read from the tables
+#endif
+#ifndef ACMMP_REF_VBA
+#define ACMMP_REF_VBA 2                     // k_eval_ref / tail: 2-view NCC chunks where launches have 4-view ones (r01_v40 A/B +1.7%)
+#endif
 constexpr int kRefLanes = 5;                // refinement candidates (ACMMP.cu:870)
 constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 lanes used)
 
@@ -1638,7 +1644,14 @@ __global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_
         vw = st.vw;
         weight_norm = st.weight_norm;
     }
+#if ACMMP_REF_LITE
+    constexpr int kStaged = 2;
+    const Patch pt = coop_patch_lite<MODEL>(kp, valid, px, py, lp, h, kRefLanes, reinterpret_cast<float2*>(lds4));
+#else
+    constexpr int kStaged = 3;
     const Patch pt = coop_patch_nb<MODEL, kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
+#endif
+    constexpr int VBA = (VB == 4 && ACMMP_REF_VBA == 2) ? 2 : (VB > kEvalVB ? kEvalVB : VB);
     if (!valid) return;
     if (kp.ref_split > 0 && h == 0) {                        // the tail's patch, without re-summing it
         const DevCam& rc = kp.cams[0];
@@ -1662,7 +1675,7 @@ __global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_
     float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
     for (int v = 0; v < kp.V; ++v)
         if (!((amask >> v) & 1u)) vcost[v * Pc] = __builtin_nanf("");
-    for_all_views<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, ACMMP_REF_PIPE>(kp, px, py, pt, tp, amask, [&](int v, float c) {
+    for_all_views<MODEL, VBA, kStaged, ACMMP_REF_PIPE>(kp, px, py, pt, tp, amask, [&](int v, float c) {
         vcost[v * Pc] = c;
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
@@ -1721,7 +1734,8 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
         pt.sbw = ps.x; pt.sref = ps.y; pt.srr = ps.z; pt.center = ps.w;
         float temp_cost = kp.cand_cost[h * Pc + ci];
         float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
-        for_all_views<MODEL, (VB > kEvalVB ? kEvalVB : VB), 0, ACMMP_REF_PIPE>(kp, px, py, pt, tp, umask, [&](int v, float c) {
+        constexpr int VBT = (VB == 4 && ACMMP_REF_VBA == 2) ? 2 : (VB > kEvalVB ? kEvalVB : VB);
+        for_all_views<MODEL, VBT, 0, ACMMP_REF_PIPE>(kp, px, py, pt, tp, umask, [&](int v, float c) {
             vcost[v * Pc] = c;
             const float w = vw_get(vwp, v);
             if (w > 0.0f) {
@@ -2021,7 +2035,7 @@ hipError_t launch_init(const KParams& kp, hipStream_t s) {
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s, hipEvent_t* ev) {
     const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
     const size_t lds_nb = nb_lds_bytes(kp.model, kp.S, kp.nside);
-    const size_t lds_ref = nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
+    const size_t lds_ref = ACMMP_REF_LITE ? sizeof(float2) * kp.S * kRefPix : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
     hipError_t e = hipSuccess;
 #define ACMMP_MARK(i) if (ev && (e = hipEventRecord(ev[i], s)) != hipSuccess) return e
     // k_pick sits outside the four timed buckets (rocprof lists it): the k_eval_nb bucket the bench's
