@@ -38,6 +38,10 @@ struct acmmp_ctx {
     DevCam* d_cams = nullptr;
     float* d_img = nullptr;
     uint16_t* d_img16 = nullptr;     // binary16 copy of d_img (null when some texel is not exact)
+    size_t img_cap = 0, img16_cap = 0;  // texels the two image allocations hold (grow-only)
+    char* d_stage = nullptr;         // upload staging for all of a problem's images (grow-only)
+    size_t stage_cap = 0;
+    int* d_flag = nullptr;           // k_to_f16's inexact flag
 
     float* d_dep = nullptr;
     bool has_depths = false;
@@ -102,6 +106,16 @@ template <typename T>
 hipError_t dalloc(T*& p, size_t count) {
     dfree(p);
     return hipMalloc(reinterpret_cast<void**>(&p), sizeof(T) * std::max<size_t>(count, 1));
+}
+
+// Grow-only allocation: reallocates only when `count` exceeds the capacity (contents not kept).
+template <typename T>
+hipError_t dreserve(T*& p, size_t& cap, size_t count) {
+    if (p && count <= cap) return hipSuccess;
+    cap = 0;
+    const hipError_t e = dalloc(p, count);
+    if (e == hipSuccess) cap = count;
+    return e;
 }
 
 size_t P_of(const acmmp_ctx* c) { return static_cast<size_t>(c->W) * c->H; }
@@ -192,6 +206,7 @@ void acmmp_destroy(acmmp_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     dfree(c->d_cams); dfree(c->d_img); dfree(c->d_img16); dfree(c->d_dep); dfree(c->d_dirs);
+    dfree(c->d_stage); dfree(c->d_flag);
     dfree(c->d_sph_row); dfree(c->d_sph_col); dfree(c->d_spatial);
     dfree(c->d_planes_rm); dfree(c->d_costs_rm); dfree(c->d_pre); dfree(c->d_sel_rm);
     dfree(c->d_scaled); dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_scratch); dfree(c->d_work);
@@ -248,44 +263,45 @@ acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images,
         total += static_cast<long long>(cams[i].width + 2) * (cams[i].height + 2);
         total = (total + 63) & ~63LL;
     }
-    HIP_TRY(c, dalloc(c->d_img, static_cast<size_t>(total)));
+    // allocations are kept across uploads (a pipeline uploads every problem of every pass); all
+    // images go through one staging buffer, copies and padding kernels back to back on the stream
+    HIP_TRY(c, dreserve(c->d_img, c->img_cap, static_cast<size_t>(total)));
     HIP_TRY(c, hipMemsetAsync(c->d_img, 0, sizeof(float) * static_cast<size_t>(total), c->stream));  // gaps between views
-    float* staging = nullptr;
-    size_t staging_cap = 0;
+    std::vector<size_t> soff(n + 1, 0);
+    for (int i = 0; i < n; ++i) {
+        const size_t rowb = sizeof(float) * cams[i].width;
+        const size_t pb = pitch_bytes ? pitch_bytes[i] : rowb;
+        soff[i + 1] = soff[i] + ((pb * (cams[i].height - 1) + rowb + 255) & ~static_cast<size_t>(255));
+    }
+    HIP_TRY(c, dreserve(c->d_stage, c->stage_cap, soff[n]));
     for (int i = 0; i < n; ++i) {
         const size_t rowb = sizeof(float) * cams[i].width;
         const size_t pb = pitch_bytes ? pitch_bytes[i] : rowb;
         const size_t bytes = pb * (cams[i].height - 1) + rowb;
-        if (bytes > staging_cap) {
-            dfree(staging);
-            HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&staging), bytes));
-            staging_cap = bytes;
-        }
+        float* staging = reinterpret_cast<float*>(c->d_stage + soff[i]);
         HIP_TRY(c, hipMemcpyAsync(staging, images[i], bytes, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(c, launch_pad_image(staging, pb / sizeof(float), cams[i].width, cams[i].height, c->d_img + off[i],
                                     cams[i].width + 2, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
     }
-    dfree(staging);
 
     // binary16 copy for the NCC fetches when it holds the same values (8-bit images always do):
     // half the bytes per footprint, so twice the views fit a cache level.
     // ACMMP_TEX16=0 in the environment keeps the fp32 fetches (A/B switch; identical results).
-    dfree(c->d_img16);
     const char* tex16_env = std::getenv("ACMMP_TEX16");
     if (!(tex16_env && tex16_env[0] == '0')) {
-        int* d_flag = nullptr;
-        HIP_TRY(c, dalloc(c->d_img16, static_cast<size_t>(total)));
-        HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&d_flag), sizeof(int)));
+        HIP_TRY(c, dreserve(c->d_img16, c->img16_cap, static_cast<size_t>(total)));
+        if (!c->d_flag) HIP_TRY(c, dalloc(c->d_flag, 1));
         int inexact = 0;
-        hipError_t e = hipMemsetAsync(d_flag, 0, sizeof(int), c->stream);
-        if (e == hipSuccess) e = launch_to_f16(c->d_img, total, c->d_img16, d_flag, c->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(&inexact, d_flag, sizeof(int), hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-        dfree(d_flag);
-        HIP_TRY(c, e);
-        if (inexact) dfree(c->d_img16);
+        HIP_TRY(c, hipMemsetAsync(c->d_flag, 0, sizeof(int), c->stream));
+        HIP_TRY(c, launch_to_f16(c->d_img, total, c->d_img16, c->d_flag, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(&inexact, c->d_flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        if (inexact) { dfree(c->d_img16); c->img16_cap = 0; }
+    } else {
+        dfree(c->d_img16);
+        c->img16_cap = 0;
     }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));          // staging and padding done before returning
 
     c->dcams.assign(n, DevCam{});
     for (int i = 0; i < n; ++i) {
