@@ -433,15 +433,12 @@ static unsigned long long colour_pixels(const acmmp_ctx* c, const KParams& kp, i
 // Split point of the refinement evaluation: about half the views, a multiple of the
 // 4-view NCC chunk above 4 views; 0 (no split) for one view, for colour grids too large for the
 // 32-bit queue entries, or with ACMMP_REF_SPLIT=0 in the environment (A/B switch).
+// Read at every run (one getenv per RunPatchMatch), so tests can switch it within one process.
 static int ref_split_point(int V, size_t Pc) {
-    static const int enabled = [] {
-        const char* e = std::getenv("ACMMP_REF_SPLIT");
-        return e ? std::atoi(e) : 1;
-    }();
-    static const int at = [] {                              // ACMMP_REF_SPLIT_AT=S: fixed split (A/B)
-        const char* e = std::getenv("ACMMP_REF_SPLIT_AT");
-        return e ? std::atoi(e) : 0;
-    }();
+    const char* e_on = std::getenv("ACMMP_REF_SPLIT");
+    const char* e_at = std::getenv("ACMMP_REF_SPLIT_AT");  // ACMMP_REF_SPLIT_AT=S: fixed split (A/B)
+    const int enabled = e_on ? std::atoi(e_on) : 1;
+    const int at = e_at ? std::atoi(e_at) : 0;
     if (!enabled || V < 2 || Pc >= (static_cast<size_t>(1) << 29)) return 0;
     if (at > 0) return at < V ? at : 0;
     return V <= 4 ? V / 2 : 4 * std::max(1, (V / 2 + 2) / 4);

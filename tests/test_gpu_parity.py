@@ -77,6 +77,26 @@ def test_full_run_bitexact(ctx, oracle_mod, kind, W, H, V):
     check(g, o)
 
 
+SPLITS = [("sphere", 100, 50, 4, "0"), ("sphere", 100, 50, 4, "1"), ("sphere", 100, 50, 4, "3"),
+          ("pinhole", 70, 45, 10, "0"), ("pinhole", 70, 45, 10, "2"), ("pinhole", 70, 45, 10, "8")]
+
+
+@pytest.mark.parametrize("kind,W,H,V,split", SPLITS, ids=[f"{k}-v{v}-S{s}" for k, w, h, v, s in SPLITS])
+def test_refinement_split_points_bitexact(ctx, oracle_mod, monkeypatch, kind, W, H, V, split):
+    """The split refinement evaluation (k_eval_ref on views [0, S), pruning, k_eval_ref_tail on the rest)
+    is exact for every split point: S = 0 (one pass over all views) and fixed S other than the default
+    all equal the oracle bit for bit -- a candidate dropped by its partial bound is never accepted."""
+    sc = make(kind, W, H, V, seed=W + V + 1)
+    if split == "0":
+        monkeypatch.setenv("ACMMP_REF_SPLIT", "0")
+    else:
+        monkeypatch.setenv("ACMMP_REF_SPLIT_AT", split)
+    p = params_for(sc)
+    g = gpu_run(ctx, sc, p, seed=777)
+    o = oracle_mod.run_patchmatch(oracle_mod.Problem(sc.images, sc.cameras, p), seed=777)
+    check(g, o)
+
+
 @pytest.mark.parametrize("kind", ["pinhole", "sphere"])
 @pytest.mark.parametrize("fmt", ["f16", "fp32-forced", "fp32-unquantized"])
 def test_texel_formats_bitexact(ctx, oracle_mod, monkeypatch, kind, fmt):
