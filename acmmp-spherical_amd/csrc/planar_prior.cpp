@@ -262,6 +262,25 @@ std::vector<int> support_points(const float* costs, int W, int H) {
     return all;
 }
 
+// GetDepthFromPlaneParam's SPHERE ray (ACMMP.cpp:993-1006) is separable: sin/cos of the latitude
+// depend on the row only and of the longitude on the column only, so a whole-image pass computes
+// them once per row / column -- the same float values the per-pixel expressions give.
+struct SphereTrig { float s, c; };
+SphereTrig sphere_row(const acmmp_camera& c, int y) {
+    const float lat = static_cast<float>(-(static_cast<float>(y) - c.params[2]) / static_cast<float>(c.height) * kMPi);
+    return {std::sin(lat), std::cos(lat)};
+}
+SphereTrig sphere_col(const acmmp_camera& c, int x) {
+    const float lon = static_cast<float>((static_cast<float>(x) - c.params[1]) / static_cast<float>(c.width) *
+                                         2.0f * kMPi);
+    return {std::sin(lon), std::cos(lon)};
+}
+float sphere_depth(const float plane[4], SphereTrig lat, SphereTrig lon) {
+    const float dx = lat.c * lon.s, dy = -lat.s, dz = lat.c * lon.c;
+    const float denom = plane[0] * dx + plane[1] * dy + plane[2] * dz;
+    return (std::abs(denom) < 1e-6f) ? 1e6f : (-plane[3] / denom);
+}
+
 }  // namespace
 
 extern "C" {
@@ -319,13 +338,8 @@ acmmp_status acmmp_prior_plane_params(const acmmp_camera* cam, const float* dept
 float acmmp_depth_from_plane_param(const acmmp_camera* cam, const float plane[4], int x, int y) {
     const acmmp_camera& c = *cam;
     if (c.model == ACMMP_SPHERE) {                          // ACMMP.cpp:993-1006
-        const float lon = static_cast<float>((static_cast<float>(x) - c.params[1]) / static_cast<float>(c.width) *
-                                             2.0f * kMPi);
-        const float lat = static_cast<float>(-(static_cast<float>(y) - c.params[2]) /
-                                             static_cast<float>(c.height) * kMPi);
-        const float dx = std::cos(lat) * std::sin(lon), dy = -std::sin(lat), dz = std::cos(lat) * std::cos(lon);
-        const float denom = plane[0] * dx + plane[1] * dy + plane[2] * dz;
-        return (std::abs(denom) < 1e-6f) ? 1e6f : (-plane[3] / denom);
+        const SphereTrig r = sphere_row(c, y), k = sphere_col(c, x);
+        return sphere_depth(plane, r, k);
     }
     // ACMMP.cpp:1008-1009 (int x - float K[2] -> float)
     return -plane[3] * c.K[0] /
@@ -387,13 +401,17 @@ acmmp_status acmmp_planar_prior_host(const acmmp_camera* cam, const float* depth
     });
     // prior depth range check (main.cpp:167-180) and CudaPlanarPriorInitialization (ACMMP.cpp:851-861);
     // every pixel is independent (mask_tri holds float labels idx + 1.0, exact below 2^24)
+    const bool sphere = cam->model == ACMMP_SPHERE;
+    std::vector<SphereTrig> lon_of(sphere ? W : 0);
+    for (int i = 0; sphere && i < W; ++i) lon_of[i] = sphere_col(*cam, i);
     parallel_for(H, [&](int j) {
+        const SphereTrig lat = sphere ? sphere_row(*cam, j) : SphereTrig{0.f, 0.f};
         for (int i = 0; i < W; ++i) {
             const size_t c = static_cast<size_t>(j) * W + i;
             uint32_t l = lab[c];
             if (l > 0) {
                 const float* pl = &plane_params[4 * static_cast<size_t>(l - 1)];
-                const float d = acmmp_depth_from_plane_param(cam, pl, i, j);
+                const float d = sphere ? sphere_depth(pl, lat, lon_of[i]) : acmmp_depth_from_plane_param(cam, pl, i, j);
                 if (!(d <= depth_max && d >= depth_min)) l = 0;
             }
             masks[c] = l;
