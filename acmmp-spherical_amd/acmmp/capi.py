@@ -30,7 +30,7 @@ EXPORTS = [
     "acmmp_debug_ncc", "acmmp_debug_geom",
     "acmmp_support_points", "acmmp_delaunay", "acmmp_prior_plane_params", "acmmp_depth_from_plane_param",
     "acmmp_planar_prior_host",
-    "acmmp_upload_depths_device", "acmmp_export_depth", "acmmp_device_alloc", "acmmp_device_free", "acmmp_memcpy",
+    "acmmp_upload_depths_device", "acmmp_upload_views_device", "acmmp_export_depth", "acmmp_device_alloc", "acmmp_device_free", "acmmp_memcpy",
     "acmmp_comm_unique_id", "acmmp_comm_create", "acmmp_comm_destroy", "acmmp_comm_broadcast",
     "acmmp_comm_allreduce_max",
     "acmmp_fusion_create", "acmmp_fusion_set_view", "acmmp_fusion_run", "acmmp_fusion_last_error",
@@ -88,6 +88,7 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_prior_plane_params.argtypes = [vp, vp, i32, i32, vp, vp]
     L.acmmp_depth_from_plane_param.argtypes = [vp, vp, i32, i32]
     L.acmmp_upload_depths_device.argtypes = [vp, i32, vp, vp, vp]
+    L.acmmp_upload_views_device.argtypes = [vp, i32, vp, vp, vp]
     L.acmmp_export_depth.argtypes = [vp, vp]
     L.acmmp_device_alloc.argtypes = [i32, C.c_size_t, C.POINTER(vp)]
     L.acmmp_device_free.argtypes = [i32, vp]
@@ -172,6 +173,15 @@ class Context:
         ptrs = (C.c_void_p * n)(*[im.ctypes.data for im in imgs])
         self._check(self.L.acmmp_upload_views(self.h, n, C.cast(ptrs, C.c_void_p), None, _p(cams)), "upload_views")
         self.N, self.H, self.W = n, imgs[0].shape[0], imgs[0].shape[1]
+
+    def upload_views_device(self, bufs, cameras):
+        """bufs: DeviceBuffer images (index 0 = reference) on this context's GPU."""
+        cams = np.frombuffer(np.ascontiguousarray(cameras, dtype=CAMERA_DTYPE).tobytes(), CAMERA_DTYPE).copy()
+        n = len(bufs)
+        ptrs = (C.c_void_p * n)(*[b.ptr for b in bufs])
+        self._check(self.L.acmmp_upload_views_device(self.h, n, C.cast(ptrs, C.c_void_p), None, _p(cams)),
+                    "upload_views_device")
+        self.N, self.H, self.W = n, bufs[0].shape[0], bufs[0].shape[1]
 
     def upload_depths(self, depths):
         ds = [np.ascontiguousarray(d, np.float32) for d in depths]

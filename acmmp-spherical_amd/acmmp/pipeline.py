@@ -309,6 +309,7 @@ class Pipeline:
         self.problems = copy.deepcopy(ds.problems)
         self.pass_index = 0
         self._scaled = {}                                   # (view, size) -> scaled image, camera
+        self._scaled_dev = {}                               # (view, size) -> its DeviceBuffer (GPU engine)
         self.passes = []
         self._pending = []
         self.stage_s = {}                                   # host wall seconds per stage (profiling)
@@ -389,7 +390,7 @@ class Pipeline:
     def _inputs(self, idx):
         prob = self.problems[idx]
         ids = [prob.ref_image_id] + list(prob.src_image_ids)
-        images, cams = [], []
+        images, cams, keys = [], [], []
         for k, vid in enumerate(ids):
             size = prob.cur_image_size if k == 0 else self.problems[vid].cur_image_size
             key = (vid, size)
@@ -398,7 +399,25 @@ class Pipeline:
             img, cam = self._scaled[key]
             images.append(img)
             cams.append(cam)
+            keys.append(key)
+        self._keys = keys
         return ids, images, np.array(cams, dtype=types.CAMERA_DTYPE)
+
+    def _upload_views(self, e, images, cams):
+        """The problem's images: with a GPU engine and device store, each view's image of one scale is
+        copied to HBM once and every problem reading it uploads it device to device."""
+        if self.store.device is None or not hasattr(e, "upload_views_device"):
+            e.upload_views(images, cams)
+            return
+        bufs = []
+        for key, img in zip(self._keys, images):
+            b = self._scaled_dev.get(key)
+            if b is None:
+                b = capi.DeviceBuffer(self.store.device, img.shape)
+                b.upload(img)
+                self._scaled_dev[key] = b
+            bufs.append(b)
+        e.upload_views_device(bufs, cams)
 
     # -- ProcessProblem (main.cpp:73-210)
     def process_problem(self, idx, geom, planar, hier, multi):
@@ -455,7 +474,7 @@ class Pipeline:
         if geom:
             key = "depths_geom" if multi else "depths"
             e.set_params(p)
-            e.upload_views(images, cams)
+            self._upload_views(e, images, cams)
             if self.store.device is not None and hasattr(e, "upload_depths_device"):
                 e.upload_depths_device([self.store.device_map(key, v) for v in ids])
             else:
@@ -479,14 +498,14 @@ class Pipeline:
                 p["upsample"] = 0
                 scaled = np.concatenate([normals, depth[..., None]], axis=-1)
             e.set_params(p)
-            e.upload_views(images, cams)
+            self._upload_views(e, images, cams)
             e.set_scaled_state(scaled)
             state = np.zeros((H, W, 4), np.float32)
             state[..., 3] = depth[:H, :W] if depth.shape == (H, W) else 0.0
             e.set_state(state, None)
         else:
             e.set_params(p)
-            e.upload_views(images, cams)
+            self._upload_views(e, images, cams)
 
     # -- RunFusionCuda (ACMMP.cu:1817-2105), after the last pass
     def run_fusion(self, fusion_factory=None, ply_path: str | None = None):

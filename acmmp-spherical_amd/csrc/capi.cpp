@@ -232,8 +232,24 @@ acmmp_status acmmp_set_params(acmmp_ctx* c, const acmmp_params* p) {
 }
 
 
+static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* images, const size_t* pitch_bytes,
+                                      const acmmp_camera* cams, bool device_src);
+
 acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images, const size_t* pitch_bytes,
                                 const acmmp_camera* cams) {
+    return upload_views_impl(c, n, images, pitch_bytes, cams, false);
+}
+
+acmmp_status acmmp_upload_views_device(acmmp_ctx* c, int n, const float* const* dev_images, const size_t* pitch_bytes,
+                                       const acmmp_camera* cams) {
+    return upload_views_impl(c, n, dev_images, pitch_bytes, cams, true);
+}
+
+}  // extern "C"
+
+// Host images go through one staging buffer; device images are padded straight from their buffers.
+static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* images, const size_t* pitch_bytes,
+                                      const acmmp_camera* cams, bool device_src) {
     if (!c || !images || !cams) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
     if (n < 2 || n > kMaxViews + 1) return fail(c, ACMMP_ERR_UNSUPPORTED, "need 2..33 images");
     for (int i = 0; i < n; ++i) {
@@ -273,14 +289,18 @@ acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images,
         const size_t pb = pitch_bytes ? pitch_bytes[i] : rowb;
         soff[i + 1] = soff[i] + ((pb * (cams[i].height - 1) + rowb + 255) & ~static_cast<size_t>(255));
     }
-    HIP_TRY(c, dreserve(c->d_stage, c->stage_cap, soff[n]));
+    if (!device_src) HIP_TRY(c, dreserve(c->d_stage, c->stage_cap, soff[n]));
     for (int i = 0; i < n; ++i) {
         const size_t rowb = sizeof(float) * cams[i].width;
         const size_t pb = pitch_bytes ? pitch_bytes[i] : rowb;
         const size_t bytes = pb * (cams[i].height - 1) + rowb;
-        float* staging = reinterpret_cast<float*>(c->d_stage + soff[i]);
-        HIP_TRY(c, hipMemcpyAsync(staging, images[i], bytes, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(c, launch_pad_image(staging, pb / sizeof(float), cams[i].width, cams[i].height, c->d_img + off[i],
+        const float* src = images[i];
+        if (!device_src) {
+            float* staging = reinterpret_cast<float*>(c->d_stage + soff[i]);
+            HIP_TRY(c, hipMemcpyAsync(staging, images[i], bytes, hipMemcpyHostToDevice, c->stream));
+            src = staging;
+        }
+        HIP_TRY(c, launch_pad_image(src, pb / sizeof(float), cams[i].width, cams[i].height, c->d_img + off[i],
                                     cams[i].width + 2, c->stream));
     }
 
@@ -370,6 +390,8 @@ static acmmp_status upload_depths(acmmp_ctx* c, int n, const float* const* depth
     c->has_depths = true;
     return ACMMP_OK;
 }
+
+extern "C" {
 
 acmmp_status acmmp_upload_depths(acmmp_ctx* c, int n, const float* const* depths, const int* w, const int* h) {
     return upload_depths(c, n, depths, w, h, hipMemcpyHostToDevice);

@@ -104,6 +104,12 @@ acmmp_status acmmp_set_params(acmmp_ctx *ctx, const acmmp_params *params);
 acmmp_status acmmp_upload_views(acmmp_ctx *ctx, int n, const float *const *images,
                                 const size_t *pitch_bytes, const acmmp_camera *cams);
 
+/* The same from device buffers of this context's GPU (in-memory pipeline: a view's image of one
+ * scale is uploaded once and every problem of every pass that reads it copies it HBM to HBM).
+ * images[i] are device pointers, otherwise as acmmp_upload_views.  No reference counterpart. */
+acmmp_status acmmp_upload_views_device(acmmp_ctx *ctx, int n, const float *const *dev_images,
+                                       const size_t *pitch_bytes, const acmmp_camera *cams);
+
 /* Geometric-consistency depth textures (ACMMP.cpp:653-678, 726-751): n depth maps,
  * depths[i] is h[i] x w[i] row-major (index 0 = reference, as the reference). */
 acmmp_status acmmp_upload_depths(acmmp_ctx *ctx, int n, const float *const *depths,

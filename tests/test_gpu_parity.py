@@ -77,6 +77,30 @@ def test_full_run_bitexact(ctx, oracle_mod, kind, W, H, V):
     check(g, o)
 
 
+@pytest.mark.parametrize("kind", ["pinhole", "sphere"])
+def test_upload_views_device_bitexact(ctx, oracle_mod, kind):
+    """acmmp_upload_views_device (images already in HBM, the pipeline's per-scale image cache) gives
+    the run acmmp_upload_views gives: both equal the oracle bit for bit."""
+    sc = make(kind, 90, 48, 3, seed=31)
+    p = params_for(sc)
+    bufs = []
+    for im in sc.images:
+        b = capi.DeviceBuffer(0, im.shape)
+        b.upload(im)
+        bufs.append(b)
+    ctx.set_params(p)
+    ctx.upload_views_device(bufs, sc.cameras)
+    ctx.run_patchmatch(55)
+    planes, costs = ctx.download()
+    g = gpu_run(ctx, sc, p, seed=55)
+    for b in bufs:
+        b.free()
+    assert_bitwise_equal(planes, g["planes"], "planes (device upload vs host upload)")
+    assert_bitwise_equal(costs, g["costs"], "costs (device upload vs host upload)")
+    o = oracle_mod.run_patchmatch(oracle_mod.Problem(sc.images, sc.cameras, p), seed=55)
+    check(g, o)
+
+
 SPLITS = [("sphere", 100, 50, 4, "0"), ("sphere", 100, 50, 4, "1"), ("sphere", 100, 50, 4, "3"),
           ("pinhole", 70, 45, 10, "0"), ("pinhole", 70, 45, 10, "2"), ("pinhole", 70, 45, 10, "8")]
 
