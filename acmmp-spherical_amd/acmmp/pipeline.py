@@ -288,8 +288,12 @@ class Pipeline:
     def __init__(self, ds: Dataset, engine=None, exchange=None, device: int = 0, seed: int = 1234,
                  order: str = "reference", geom_iterations: int = 2, out_folder: str | None = None,
                  use_device_store: bool | None = None, size_bound: int = 1000, max_image_size: int = 3200,
-                 log=None):
+                 log=None, reuse_planes: bool = True):
         self.ds = ds
+        # a geom pass restarts from the previous pass's depth + normals of its view, which is that
+        # pass's downloaded plane array: keep it instead of re-joining the two stored maps
+        self.reuse_planes = reuse_planes
+        self._last_planes = {}                              # view -> (H, W, 4) planes of its last pass
         self.exchange = exchange or LocalExchange()
         self.world, self.rank = self.exchange.world, self.exchange.rank
         if self.world > 1 and order == "reference":
@@ -460,6 +464,7 @@ class Pipeline:
             self._save(key, ref, planes[..., 3].copy(), e if isinstance(e, capi.Context) else None)
             self.store.put("normals", ref, planes[..., :3].copy())
             self.store.put("costs", ref, costs)
+            self._last_planes[ref] = planes
             if self.out_folder:
                 d = os.path.join(self.out_folder, "ACMMP", f"2333_{ref:08d}")
                 os.makedirs(d, exist_ok=True)
@@ -479,10 +484,12 @@ class Pipeline:
                 e.upload_depths_device([self.store.device_map(key, v) for v in ids])
             else:
                 e.upload_depths([self.store.get(key, v) for v in ids])
-            depth = self.store.get(key, ref)
-            normals = self.store.get("normals", ref)
             costs = self.store.get("costs", ref)
-            planes = np.concatenate([normals, depth[..., None]], axis=-1)
+            planes = self._last_planes.get(ref) if self.reuse_planes else None
+            if planes is None or planes.shape[:2] != (H, W):
+                depth = self.store.get(key, ref)
+                normals = self.store.get("normals", ref)
+                planes = np.concatenate([normals, depth[..., None]], axis=-1)
             e.set_state(planes, costs)
         elif hier:
             depth = self.store.get("depths", ref)                    # JBU output, fine size

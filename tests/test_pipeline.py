@@ -49,6 +49,20 @@ def test_pipeline_schedule_single_rank():
         assert pipe.store.get("depths", v).shape == (32, 64)         # JBU output / hier-planar pass
 
 
+@pytest.mark.parametrize("order", ["reference", "snapshot"])
+def test_geom_pass_state_reuse_equals_rejoined_maps(order):
+    """A geom pass restarts from its view's previous-pass planes: reusing that pass's downloaded plane
+    array gives exactly the run that re-joins the stored depth and normal maps (ProcessProblem's
+    reload, main.cpp:87-97), over the two-scale schedule."""
+    a = pipeline.Pipeline(small_dataset(64, 32, 3), engine=OracleEngine(), order=order, size_bound=40,
+                          reuse_planes=True).run()
+    b = pipeline.Pipeline(small_dataset(64, 32, 3), engine=OracleEngine(), order=order, size_bound=40,
+                          reuse_planes=False).run()
+    for key in ("depths", "depths_geom", "normals", "costs"):
+        for v in range(3):
+            assert_bitwise_equal(a.store.get(key, v), b.store.get(key, v), f"{key} view {v}")
+
+
 def test_pipeline_writes_reference_layout(tmp_path):
     ds = small_dataset(48, 24, 2)
     pipeline.Pipeline(ds, engine=OracleEngine(), order="reference", geom_iterations=1,
