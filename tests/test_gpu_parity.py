@@ -232,6 +232,25 @@ def test_geom_consistency_pass_bitexact(ctx, oracle_mod, kind):
 
 
 @pytest.mark.parametrize("kind", ["pinhole", "sphere"])
+@pytest.mark.parametrize("split", ["1", "3"])
+def test_geom_pass_split_points_bitexact(ctx, oracle_mod, monkeypatch, kind, split):
+    """The refinement split in a geom pass (the pruned aggregate carries w * (c + 0.1 geom) terms) at
+    non-default split points, four source views: bit-exact."""
+    sc = make(kind, 72, 48, 4, seed=37)
+    p0 = params_for(sc)
+    first = oracle_mod.run_patchmatch(oracle_mod.Problem(sc.images, sc.cameras, p0), seed=3)
+    rng = np.random.default_rng(5)
+    depths = [first["planes"][..., 3]] + [first["planes"][..., 3] * rng.uniform(0.97, 1.03, (48, 72)).astype(np.float32)
+                                          for _ in range(4)]
+    monkeypatch.setenv("ACMMP_REF_SPLIT_AT", split)
+    pg = params_for(sc, geom_consistency=1, max_iterations=2)
+    g = gpu_run(ctx, sc, pg, seed=4, planes=first["planes"], costs=first["costs"], depths=depths)
+    o = oracle_mod.run_patchmatch(oracle_mod.Problem(sc.images, sc.cameras, pg, depths=depths), seed=4,
+                                  planes=first["planes"], costs=first["costs"])
+    check(g, o)
+
+
+@pytest.mark.parametrize("kind", ["pinhole", "sphere"])
 @pytest.mark.parametrize("geom", [0, 1])
 def test_planar_prior_pass_bitexact(ctx, oracle_mod, kind, geom):
     """Second RunPatchMatch of ProcessProblem (main.cpp:113-197) on device-resident state:
