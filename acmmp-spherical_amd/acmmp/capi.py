@@ -166,9 +166,24 @@ class Context:
         self._params = p
         self._check(self.L.acmmp_set_params(self.h, _p(p)), "set_params")
 
+    @staticmethod
+    def _check_view_shapes(shapes, cams):
+        """The C side sizes every copy from the cameras: a mismatched array would be read past its end."""
+        if len(shapes) != len(cams):
+            raise ValueError(f"{len(shapes)} images for {len(cams)} cameras")
+        for i, (shp, cam) in enumerate(zip(shapes, cams)):
+            if tuple(shp) != (int(cam["height"]), int(cam["width"])):
+                raise ValueError(f"image {i} has shape {tuple(shp)}, camera says {int(cam['height'])}x{int(cam['width'])}")
+
+    def _check_hw(self, arr, tail, what):
+        want = (self.H, self.W) + tail
+        if arr.shape != want and arr.size != int(np.prod(want)):
+            raise ValueError(f"{what}: shape {arr.shape}, expected {want}")
+
     def upload_views(self, images, cameras):
         imgs = [np.ascontiguousarray(im, np.float32) for im in images]
         cams = np.frombuffer(np.ascontiguousarray(cameras, dtype=CAMERA_DTYPE).tobytes(), CAMERA_DTYPE).copy()
+        self._check_view_shapes([im.shape for im in imgs], cams)
         n = len(imgs)
         ptrs = (C.c_void_p * n)(*[im.ctypes.data for im in imgs])
         self._check(self.L.acmmp_upload_views(self.h, n, C.cast(ptrs, C.c_void_p), None, _p(cams)), "upload_views")
@@ -177,6 +192,7 @@ class Context:
     def upload_views_device(self, bufs, cameras):
         """bufs: DeviceBuffer images (index 0 = reference) on this context's GPU."""
         cams = np.frombuffer(np.ascontiguousarray(cameras, dtype=CAMERA_DTYPE).tobytes(), CAMERA_DTYPE).copy()
+        self._check_view_shapes([tuple(b.shape[:2]) for b in bufs], cams)
         n = len(bufs)
         ptrs = (C.c_void_p * n)(*[b.ptr for b in bufs])
         self._check(self.L.acmmp_upload_views_device(self.h, n, C.cast(ptrs, C.c_void_p), None, _p(cams)),
@@ -207,6 +223,10 @@ class Context:
     def set_state(self, planes=None, costs=None):
         pl = None if planes is None else np.ascontiguousarray(planes, np.float32)
         co = None if costs is None else np.ascontiguousarray(costs, np.float32)
+        if pl is not None:
+            self._check_hw(pl, (4,), "set_state planes")
+        if co is not None:
+            self._check_hw(co, (), "set_state costs")
         self._check(self.L.acmmp_set_state(self.h, _p(pl), _p(co)), "set_state")
 
     def set_scaled_state(self, planes):
@@ -216,6 +236,8 @@ class Context:
     def set_planar_prior(self, prior_planes, masks):
         pr = np.ascontiguousarray(prior_planes, np.float32)
         mk = np.ascontiguousarray(masks, np.uint32)
+        self._check_hw(pr, (4,), "set_planar_prior planes")
+        self._check_hw(mk, (), "set_planar_prior masks")
         self._check(self.L.acmmp_set_planar_prior(self.h, _p(pr), _p(mk)), "set_planar_prior")
 
     # -- run
@@ -228,6 +250,13 @@ class Context:
         costs = np.empty((self.H, self.W), np.float32)
         self._check(self.L.acmmp_download(self.h, _p(planes), _p(costs)), "download")
         return planes, costs
+
+    def download_into(self, planes, costs):
+        """D2H into caller-owned C-contiguous float32 arrays (H, W, 4) and (H, W)."""
+        for a, tail in ((planes, (4,)), (costs, ())):
+            if a.dtype != np.float32 or not a.flags.c_contiguous or a.shape != (self.H, self.W) + tail:
+                raise ValueError("download_into: need C-contiguous float32 (H, W, 4) planes and (H, W) costs")
+        self._check(self.L.acmmp_download(self.h, _p(planes), _p(costs)), "download")
 
     def download_aux(self):
         sel = np.empty((self.H, self.W), np.uint32)

@@ -186,6 +186,14 @@ def fusion_inputs(ds: "Dataset", store, problems):
     return np.array(cams, dtype=types.CAMERA_DTYPE), depths, normals, colours
 
 
+def scaled_dims(rows: int, cols: int, max_image_size: int):
+    """(rows, cols) after InuputInitialization's rescale (ACMMP.cpp:607-617): float32 factor, rounded."""
+    if cols <= max_image_size and rows <= max_image_size:
+        return rows, cols
+    factor = min(np.float32(max_image_size) / np.float32(cols), np.float32(max_image_size) / np.float32(rows))
+    return int(np.round(np.float32(rows) * factor)), int(np.round(np.float32(cols) * factor))
+
+
 def scale_view(image: np.ndarray, cam: np.ndarray, max_image_size: int):
     """InuputInitialization's per-view rescale (ACMMP.cpp:607-643): only when the image exceeds
     max_image_size; SPHERE scales (cx, cy), PINHOLE scales K."""
@@ -193,9 +201,7 @@ def scale_view(image: np.ndarray, cam: np.ndarray, max_image_size: int):
     rows, cols = image.shape
     if cols <= max_image_size and rows <= max_image_size:
         return image, cam
-    factor = min(np.float32(max_image_size) / np.float32(cols), np.float32(max_image_size) / np.float32(rows))
-    new_cols = int(np.round(np.float32(cols) * factor))
-    new_rows = int(np.round(np.float32(rows) * factor))
+    new_rows, new_cols = scaled_dims(rows, cols, max_image_size)
     sx = np.float32(new_cols) / np.float32(cols)
     sy = np.float32(new_rows) / np.float32(rows)
     out = resize_linear(image, new_cols, new_rows)
@@ -355,6 +361,7 @@ class Pipeline:
                 if p.num_downscale >= 0:
                     p.cur_image_size = int(p.max_image_size / (2 ** p.num_downscale))
                     p.num_downscale -= 1
+            self._evict_scaled()
             if flag == 0:
                 flag = 1
                 self._pass(geom=False, planar=True, hier=False, multi=False)
@@ -387,8 +394,15 @@ class Pipeline:
         self.pass_index += 1
 
     def _pass_shape(self, view_id):
-        img, _ = scale_view(self.ds.images[view_id], self.ds.cameras[view_id], self.problems[view_id].cur_image_size)
-        return img.shape
+        rows, cols = self.ds.images[view_id].shape[:2]
+        return scaled_dims(rows, cols, self.problems[view_id].cur_image_size)
+
+    def _evict_scaled(self):
+        """Drop the rescaled images (host and HBM) of sizes no view uses any more."""
+        for key in [k for k in self._scaled if k[1] != self.problems[k[0]].cur_image_size]:
+            del self._scaled[key]
+        for key in [k for k in self._scaled_dev if k[1] != self.problems[k[0]].cur_image_size]:
+            self._scaled_dev.pop(key).free()
 
     def _commit_pending(self):
         for key, view, arr, ctx in self._pending:

@@ -1,7 +1,7 @@
 """POD types of the drop-in boundary, as numpy dtypes.
 
 Byte-for-byte the reference's ABI structs:
-  Camera           /root/reference/main.h:189-203   (120 bytes)
+  Camera           /root/reference/main.h:40-54   (120 bytes)
   PatchMatchParams /root/reference/ACMMP.h:32-55    (68 bytes)
 and the C declarations in include/acmmp.h (acmmp_camera, acmmp_params).
 """

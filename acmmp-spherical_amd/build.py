@@ -1,13 +1,19 @@
 """Build the in-tree HIP extension libacmmp.so for gfx950 (no cmake; plain hipcc).
 
 `python acmmp-spherical_amd/build.py` or `acmmp.build.build()`; __graft_entry__.build()
-calls it.  Objects are rebuilt only when a source or header is newer than the .so.
+calls it with force=True (every object recompiled, in parallel).  Without force, objects are rebuilt
+only when a source or header is newer than them.  Every link writes `acmmp/build_info.json` (sources'
+SHA-256, compiler flags, UTC time) next to the library, so a run can show which build it loaded.
 """
 from __future__ import annotations
 
+import datetime
+import hashlib
+import json
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
@@ -36,23 +42,35 @@ def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines=(),
         return lib
     objdir = objdir or os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
-    objs = []
+    objs, cmds = [], []
     for src in SOURCES:
         obj = os.path.join(objdir, src + ".o")
         srcp = os.path.join(CSRC, src)
         hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "acmmp.h")]
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < _newest([srcp] + hdrs):
             lang = ["-x", "hip"] if src in HIP_CPP else []
-            cmd = [HIPCC, *COMMON, *flags, *[f"-D{d}" for d in defines], *lang, "-c", srcp, "-o", obj]
-            if verbose:
-                print("[acmmp build]", " ".join(cmd), flush=True)
-            subprocess.run(cmd, check=True)
+            cmds.append([HIPCC, *COMMON, *flags, *[f"-D{d}" for d in defines], *lang, "-c", srcp, "-o", obj])
         objs.append(obj)
+
+    def compile_one(cmd):
+        if verbose:
+            print("[acmmp build]", " ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+
+    with ThreadPoolExecutor(max_workers=min(len(cmds), 4) or 1) as ex:
+        list(ex.map(compile_one, cmds))
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs, "-L/opt/rocm/lib", "-lrccl",
            "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print("[acmmp build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    info = {"library": os.path.basename(lib), "built_utc": datetime.datetime.now(datetime.timezone.utc).isoformat(),
+            "forced": bool(force), "arch": ARCH, "flags": COMMON + list(flags), "defines": list(defines),
+            "sources_sha256": {os.path.relpath(d, os.path.dirname(HERE)): hashlib.sha256(open(d, "rb").read()).hexdigest()
+                               for d in deps}}
+    with open(os.path.join(os.path.dirname(lib), "build_info.json" if lib == LIB else
+                           os.path.basename(lib) + ".build_info.json"), "w") as f:
+        json.dump(info, f, indent=1)
     return lib
 
 

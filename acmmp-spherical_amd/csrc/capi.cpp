@@ -20,7 +20,7 @@
 
 using namespace acmmp;
 
-static_assert(sizeof(acmmp_camera) == 120, "Camera layout (main.h:189-203)");
+static_assert(sizeof(acmmp_camera) == 120, "Camera layout (main.h:40-54)");
 static_assert(sizeof(acmmp_params) == 68, "PatchMatchParams layout (ACMMP.h:32-55)");
 static_assert(offsetof(acmmp_params, scaled_cols) == 52, "PatchMatchParams layout");
 static_assert(offsetof(acmmp_params, geom_consistency) == 60, "PatchMatchParams layout");
@@ -60,9 +60,11 @@ struct acmmp_ctx {
 
     float4* d_scaled = nullptr;
     int sw = 0, sh = 0;
+    bool has_scaled = false;          // set_scaled_state since the last upload_views
 
     float4* d_prior = nullptr;
     uint32_t* d_mask = nullptr;
+    bool has_prior = false;           // set_planar_prior since the last upload_views
 
     float4* d_plane_cs[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
     float* d_cost_cs[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
@@ -264,6 +266,10 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
     }
     HIP_TRY(c, hipSetDevice(c->device));
     const bool resized = (c->W != cams[0].width || c->H != cams[0].height);
+    // a new problem: the previous problem's prior / scaled state no longer applies (the reference
+    // builds a fresh ACMMP object per ProcessProblem, main.cpp:80)
+    c->has_prior = false;
+    c->has_scaled = false;
     c->N = n;
     c->W = cams[0].width;
     c->H = cams[0].height;
@@ -349,7 +355,6 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
         HIP_TRY(c, dalloc(c->d_sel_rm, P));
         HIP_TRY(c, hipMemset(c->d_planes_rm, 0, sizeof(float4) * P));
         HIP_TRY(c, hipMemset(c->d_costs_rm, 0, sizeof(float) * P));
-        HIP_TRY(c, hipMemset(c->d_pre, 0, sizeof(float) * P));   // never written outside the upsample branch
         HIP_TRY(c, hipMemset(c->d_sel_rm, 0, sizeof(uint32_t) * P));
         for (int k = 0; k < 2; ++k) {
             for (int b = 0; b < 2; ++b) {
@@ -363,6 +368,11 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
         dfree(c->d_scratch);
         c->scratch_bytes = 0;
     }
+    // pre_costs are written only by the upsample branch (ACMMP.cu:776) and otherwise read as zero
+    // (DESIGN.md §2.2): zero them for every problem so a context reused across problems never leaks
+    // another view's costs into k_finish's hierarchy gate
+    HIP_TRY(c, hipMemsetAsync(c->d_pre, 0, sizeof(float) * P_of(c), c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     return ACMMP_OK;
 }
 
@@ -427,6 +437,7 @@ acmmp_status acmmp_set_scaled_state(acmmp_ctx* c, const float* planes, int sw, i
     HIP_TRY(c, hipMemcpy(c->d_scaled, planes, sizeof(float4) * sw * sh, hipMemcpyHostToDevice));
     c->sw = sw;
     c->sh = sh;
+    c->has_scaled = true;
     return ACMMP_OK;
 }
 
@@ -439,6 +450,7 @@ acmmp_status acmmp_set_planar_prior(acmmp_ctx* c, const float* prior, const uint
     HIP_TRY(c, dalloc(c->d_mask, P));
     HIP_TRY(c, hipMemcpy(c->d_prior, prior, sizeof(float4) * P, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(c->d_mask, masks, sizeof(uint32_t) * P, hipMemcpyHostToDevice));
+    c->has_prior = true;
     return ACMMP_OK;
 }
 
@@ -472,8 +484,8 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
     if (p.num_images != c->N) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "params.num_images != uploaded images");
     if (p.geom_consistency && !c->has_depths) return fail(c, ACMMP_ERR_STATE, "geom_consistency needs upload_depths");
-    if (p.planar_prior && (!c->d_prior || !c->d_mask)) return fail(c, ACMMP_ERR_STATE, "planar_prior needs set_planar_prior");
-    if (!p.geom_consistency && p.hierarchy && !p.planar_prior && !c->d_scaled)
+    if (p.planar_prior && !c->has_prior) return fail(c, ACMMP_ERR_STATE, "planar_prior needs set_planar_prior");
+    if (!p.geom_consistency && p.hierarchy && !p.planar_prior && !c->has_scaled)
         return fail(c, ACMMP_ERR_STATE, "hierarchy needs set_scaled_state");
     if (p.upsample && !p.planar_prior && p.hierarchy &&
         (c->sw != static_cast<int>(p.scaled_cols) || c->sh != static_cast<int>(p.scaled_rows)))

@@ -16,7 +16,7 @@
 
 namespace acmmp_host {
 
-using Camera = acmmp_camera;                 // main.h:189-203
+using Camera = acmmp_camera;                 // main.h:40-54
 using PatchMatchParams = acmmp_params;       // ACMMP.h:32-55
 
 struct Float4 { float x, y, z, w; };         // the reference's float4 plane hypothesis

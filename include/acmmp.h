@@ -10,7 +10,7 @@
  * Threading: one context = one GPU = one host thread at a time (the reference is
  * single-threaded and not re-entrant either).  All host pointers are borrowed for
  * the duration of the call.  Errors are returned as acmmp_status codes; the C++
- * facade (acmmp-spherical_amd/host/ACMMP.h) maps them to the reference's
+ * facade (acmmp-spherical_amd/host/ACMMP.hpp) maps them to the reference's
  * print-and-exit behaviour of CUDA_SAFE_CALL (ACMMP.cpp:64-72).
  */
 #ifndef ACMMP_C_ABI_H
@@ -29,7 +29,7 @@ extern "C" {
 #define ACMMP_PINHOLE 0
 #define ACMMP_SPHERE 11
 
-/* Camera, main.h:189-203 -- identical layout (120 bytes). */
+/* Camera, main.h:40-54 -- identical layout (120 bytes). */
 typedef struct acmmp_camera {
     int32_t model;          /* ACMMP_PINHOLE or ACMMP_SPHERE */
     float params[4];        /* SPHERE: f, cx, cy, unused */

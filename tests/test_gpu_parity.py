@@ -309,14 +309,18 @@ def test_hierarchy_upsample_bitexact(ctx, oracle_mod, kind):
     o = oracle_mod.run_patchmatch(oracle_mod.Problem(fine.images, fine.cameras, p, scaled_planes=coarse), seed=9,
                                   planes=cur)
     check(g, o, keys=("planes", "costs", "selected_views", "pre_costs"))
-    # reuse branch (hierarchy at the same size, ACMMP.cu:780-793)
+    # reuse branch (hierarchy at the same size, ACMMP.cu:780-793) on the SAME context right after the
+    # upsampled problem: pre_costs are zero for the new problem (a fresh ACMMP object per problem in the
+    # reference, main.cpp:80), never the previous problem's upsample costs
+    assert np.any(g["pre_costs"] != 0)
     same = np.zeros((H, W, 4), np.float32)
     same[..., 2] = -1.0
     same[..., 3] = jbu_depth
     p2 = params_for(fine, hierarchy=1)
     g = gpu_run(ctx, fine, p2, seed=10, planes=cur, scaled=same)
     o = oracle_mod.run_patchmatch(oracle_mod.Problem(fine.images, fine.cameras, p2, scaled_planes=same), seed=10,
-                                  planes=cur, pre_costs=g["pre_costs"])
+                                  planes=cur)
+    assert not np.any(g["pre_costs"])
     check(g, o)
 
 
@@ -355,6 +359,23 @@ def test_api_errors(ctx):
     bad["model"][1] = types.SPHERE
     with pytest.raises(capi.AcmmpError, match="mixed camera models"):
         fresh.upload_views(sc.images, bad)
+    # prior / scaled state belong to one problem: a new upload_views invalidates them
+    H, W = sc.images[0].shape
+    fresh.set_params(params_for(sc))
+    fresh.upload_views(sc.images, sc.cameras)
+    fresh.set_planar_prior(np.zeros((H, W, 4), np.float32), np.zeros((H, W), np.uint32))
+    fresh.set_scaled_state(np.zeros((H, W, 4), np.float32))
+    fresh.upload_views(sc.images, sc.cameras)
+    fresh.set_params(params_for(sc, planar_prior=1))
+    with pytest.raises(capi.AcmmpError, match="set_planar_prior"):
+        fresh.run_patchmatch(1)
+    fresh.set_params(params_for(sc, hierarchy=1))
+    with pytest.raises(capi.AcmmpError, match="set_scaled_state"):
+        fresh.run_patchmatch(1)
+    with pytest.raises(ValueError, match="shape"):
+        fresh.upload_views([im[:-1] for im in sc.images], sc.cameras)
+    with pytest.raises(ValueError, match="set_planar_prior"):
+        fresh.set_planar_prior(np.zeros((H + 1, W, 4), np.float32), np.zeros((H, W), np.uint32))
     fresh.close()
 
 
