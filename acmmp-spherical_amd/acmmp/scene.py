@@ -64,7 +64,7 @@ def _plane_hit(o: np.ndarray, d: np.ndarray, n: np.ndarray, c: float) -> np.ndar
 
 def pinhole_scene(width: int = 640, height: int = 480, n_src: int = 1, seed: int = 0,
                   depth: float = 5.0, slant=(0.15, 0.08), baseline: float = 0.5,
-                  quantize: bool = True) -> Scene:
+                  quantize: bool = True, n_waves: int = 48) -> Scene:
     """Slanted textured plane z = depth + sx*x + sy*y in front of a pinhole rig."""
     f = 0.8 * width
     K = np.array([[f, 0, width / 2.0], [0, f, height / 2.0], [0, 0, 1]], np.float64)
@@ -89,7 +89,7 @@ def pinhole_scene(width: int = 640, height: int = 480, n_src: int = 1, seed: int
         d = rays_cam @ R            # world direction = R^T ray_cam  (row-vector form)
         t = _plane_hit(C, d, n, c)
         P = C + t[..., None] * d
-        img = _texture(P, seed, fmin=fmin, fmax=fmax)
+        img = _texture(P, seed, n_waves=n_waves, fmin=fmin, fmax=fmax)
         if quantize:
             img = np.round(img)
         imgs.append(img.astype(np.float32))
@@ -125,7 +125,7 @@ def sphere_dirs(width: int, height: int, cx: float, cy: float, xs=None, ys=None)
 
 
 def sphere_scene(width: int = 2000, height: int = 1000, n_src: int = 4, seed: int = 0,
-                 half=(5.0, 3.0, 4.0), baseline: float = 0.35, quantize: bool = True) -> Scene:
+                 half=(5.0, 3.0, 4.0), baseline: float = 0.35, quantize: bool = True, n_waves: int = 48) -> Scene:
     """Equirectangular rig inside a textured box room; sources displaced by ~`baseline`."""
     half = np.asarray(half, np.float64)
     cx, cy = width / 2.0, height / 2.0
@@ -148,7 +148,7 @@ def sphere_scene(width: int = 2000, height: int = 1000, n_src: int = 4, seed: in
         d = dirs_cam @ R
         t = _box_hit(C, d, half)
         P = C + t[..., None] * d
-        img = _texture(P, seed, fmin=fmin, fmax=fmax)
+        img = _texture(P, seed, n_waves=n_waves, fmin=fmin, fmax=fmax)
         if quantize:
             img = np.round(img)
         imgs.append(img.astype(np.float32))

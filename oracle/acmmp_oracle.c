@@ -521,9 +521,12 @@ static void init_pixel(const Ctx *cx, or_state *st, int x, int y, or_rng *rs)
     }
 }
 
-/* ---- PlaneHypothesisRefinement, ACMMP.cu:797-936 ---- */
+static or_trace *g_trace = NULL;
+void or_set_trace(or_trace *trace) { g_trace = trace; }
+
+/* ---- PlaneHypothesisRefinement, ACMMP.cu:797-936 (*which <- 9 + accepted candidate) ---- */
 static void refine(const Ctx *cx, f4 *plane, float *depth, float *cost, or_rng *rs,
-                   const float *vw, float weight_norm, float *restricted_cost, int px, int py)
+                   const float *vw, float weight_norm, float *restricted_cost, int px, int py, int *which)
 {
     if (weight_norm <= 0.0f) return;
     const or_params *pp = cx->pp;
@@ -594,10 +597,10 @@ static void refine(const Ctx *cx, f4 *plane, float *depth, float *cost, or_rng *
             const float prior_w = fmaf(dm_expf((-ddiff) * ddiff / two_dss), dm_expf((-ad) * ad / two_ass), gamma);
             const float rtc = dm_expf((-temp_cost) * temp_cost / beta) * prior_w;
             if (rtc > *restricted_cost) {
-                *depth = depth_before; *plane = tp; *cost = temp_cost; *restricted_cost = rtc;
+                *depth = depth_before; *plane = tp; *cost = temp_cost; *restricted_cost = rtc; *which = 9 + i;
             }
         } else if (temp_cost < *cost) {
-            *depth = depth_before; *plane = tp; *cost = temp_cost;
+            *depth = depth_before; *plane = tp; *cost = temp_cost; *which = 9 + i;
         }
     }
 }
@@ -630,6 +633,7 @@ static void propagate_pixel(const Ctx *cx, const or_state *in, or_state *out, or
     const int N = pp->num_images;
     const int center = py * width + px;
     const float *costs = in->costs;
+    const uint32_t draws_before = rs->n;
     int up_near = center - width, up_far = center - 3 * width;
     int down_near = center + width, down_far = center + 3 * width;
     int left_near = center - 1, left_far = center - 3;
@@ -819,6 +823,7 @@ static void propagate_pixel(const Ctx *cx, const or_state *in, or_state *out, or
     uint32_t cur_sel = in->selected_views[center];
     float depth_now = depth_from_plane(rc, cur_plane, px, py);
     float restricted_cost = 0.0f;
+    int max_idx_tr = -1, accepted = 8;
 
     if (pp->planar_prior) {                                     /* :1247-1299 */
         float rfc[8] = { 0 };
@@ -843,6 +848,7 @@ static void propagate_pixel(const Ctx *cx, const or_state *in, or_state *out, or
                 }
             }
             const int max_idx = find_max_idx(rfc, 8);
+            max_idx_tr = max_idx;
             const float dn = depth_from_plane(rc, cur_plane, px, py);
             const float ddiff = dn - depth_prior;
             const float ac = dot3(prior.x, prior.y, prior.z, cur_plane.x, cur_plane.y, cur_plane.z);
@@ -858,6 +864,7 @@ static void propagate_pixel(const Ctx *cx, const or_state *in, or_state *out, or
                     cur_cost = final_costs[max_idx];
                     restricted_cost = rfc[max_idx];
                     cur_sel = temp_sel;
+                    accepted = max_idx;
                 }
             }
         } else if (flag[min_idx]) {
@@ -867,6 +874,7 @@ static void propagate_pixel(const Ctx *cx, const or_state *in, or_state *out, or
                 depth_now = db;
                 cur_plane = nb;
                 cur_cost = final_costs[min_idx];
+                accepted = min_idx;
             }
         }
     }
@@ -880,10 +888,24 @@ static void propagate_pixel(const Ctx *cx, const or_state *in, or_state *out, or
             plane_now = nb;
             cost_now = final_costs[min_idx];
             cur_sel = temp_sel;
+            accepted = min_idx;
         }
     }
+    const float cost_now_cur = cost_now;
 
-    refine(cx, &plane_now, &depth_now, &cost_now, rs, vw, weight_norm, &restricted_cost, px, py);
+    refine(cx, &plane_now, &depth_now, &cost_now, rs, vw, weight_norm, &restricted_cost, px, py, &accepted);
+    if (g_trace) {
+        or_trace *t = &g_trace[center];
+        for (int d = 0; d < 8; ++d) { t->pos[d] = flag[d] ? positions[d] : -1; t->final_costs[d] = final_costs[d]; }
+        t->cost_now = cost_now_cur;
+        t->min_idx = min_idx;
+        t->max_idx = max_idx_tr;
+        t->accepted = accepted;
+        t->temp_selected_views = temp_sel;
+        t->draws_before = draws_before;
+        t->draws_after = rs->n;
+        for (int v = 0; v < 32; ++v) t->view_weights[v] = (uint8_t)vw[v];
+    }
 
     if (pp->hierarchy) {                                        /* :1315-1324 */
         if (cost_now < in->pre_costs[center] - 0.1f) {

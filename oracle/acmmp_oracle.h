@@ -31,7 +31,7 @@ extern "C" {
 
 enum { OR_PINHOLE = 0, OR_SPHERE = 11 };
 
-/* Same layout as the reference's Camera (main.h:189-203), 120 bytes. */
+/* Same layout as the reference's Camera (main.h:40-54), 120 bytes. */
 typedef struct or_camera {
     int32_t model;
     float params[4];
@@ -117,6 +117,22 @@ void or_jbu(const float *ref, int32_t W, int32_t H, const float *coarse, int32_t
  * out: 9 floats per consistent pixel, pixel order; returns the count (out may be NULL to count). */
 int32_t or_fuse(int32_t n, const or_camera *cams, const float *const *depths, const float *const *normals,
                 const float *const *rgba, int32_t ref, int32_t n_src, const int32_t *srcs, float *out);
+
+/* Per-pixel trace of the half-sweeps of the next or_run_patchmatch / or_run_band (tests only):
+ * trace[center] is (over)written by every half-sweep that updates the pixel, so after a run it
+ * holds the pixel's last update.  NULL disables tracing (the default). */
+typedef struct or_trace {
+    int32_t pos[8];                     /* picked neighbour (row-major index) per direction, -1 = flag false */
+    float final_costs[8];               /* aggregated cost per direction (:1210-1228) */
+    float cost_now;                     /* aggregated cost of the current plane (:1232-1244) */
+    int32_t min_idx, max_idx;           /* FindMinCostIndex; FindMaxCostIndex of the prior branch or -1 */
+    int32_t accepted;                   /* hypothesis left in plane_hypotheses_now: 0-7 neighbour, 8 own plane
+                                           (after the prior branch), 9+k refinement candidate k */
+    uint32_t temp_selected_views;
+    uint32_t draws_before, draws_after; /* RNG draw counter around the pixel's update */
+    uint8_t view_weights[32];           /* the 15 draws' counts per view */
+} or_trace;
+void or_set_trace(or_trace *trace);
 
 /* elementary functions and RNG, exported for tests */
 void or_detmath_eval(int32_t fn, const float *x, const float *y, float *out, int64_t n);

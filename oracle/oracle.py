@@ -72,6 +72,7 @@ def lib():
         L.or_philox.argtypes = [vp, vp, vp]
         L.or_uniform_draw.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
         L.or_uniform_draw.restype = f32
+        L.or_set_trace.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -139,6 +140,26 @@ def run_patchmatch(prob: Problem, seed: int, planes=None, costs=None, pre_costs=
     if rc != 0:
         raise RuntimeError(f"or_run_patchmatch failed ({rc})")
     return {"planes": planes, "costs": costs, "pre_costs": pre, "selected_views": sel}
+
+
+TRACE_DTYPE = np.dtype([("pos", "<i4", (8,)), ("final_costs", "<f4", (8,)), ("cost_now", "<f4"),
+                        ("min_idx", "<i4"), ("max_idx", "<i4"), ("accepted", "<i4"),
+                        ("temp_selected_views", "<u4"), ("draws_before", "<u4"), ("draws_after", "<u4"),
+                        ("view_weights", "u1", (32,))])
+
+
+def run_patchmatch_traced(prob: Problem, seed: int, **kw):
+    """run_patchmatch plus the per-pixel trace of each pixel's last half-sweep update (or_trace)."""
+    H, W = prob.shape
+    tr = np.zeros((H, W), TRACE_DTYPE)
+    tr["min_idx"] = -2
+    lib().or_set_trace(tr.ctypes.data)
+    try:
+        out = run_patchmatch(prob, seed, **kw)
+    finally:
+        lib().or_set_trace(None)
+    out["trace"] = tr
+    return out
 
 
 def run_band(prob: Problem, seed: int, row0: int, row1: int, nthreads: int = 0, n_half_sweeps: int = -1):

@@ -9,7 +9,8 @@ from acmmp import io, pipeline, scene, types
 
 class OracleEngine:
     """The capi.Context surface the pipeline uses, computed by the CPU oracle.  State persists
-    between runs exactly as the engine's does (zeroed only when the reference size changes)."""
+    between runs exactly as the engine's does (planes/costs zeroed only when the reference size
+    changes, pre_costs and the prior / scaled state reset by every upload)."""
 
     def __init__(self, nthreads: int = 8):
         self.nthreads = nthreads
@@ -27,9 +28,9 @@ class OracleEngine:
             H, W = shape
             self.planes = np.zeros((H, W, 4), np.float32)
             self.costs = np.zeros((H, W), np.float32)
-            self.pre = np.zeros((H, W), np.float32)
             self.sel = np.zeros((H, W), np.uint32)
             self.shape = shape
+        self.pre = np.zeros(shape, np.float32)             # per problem, as the engine
         self.depths = self.scaled = self.prior = self.masks = None
 
     def upload_depths(self, depths):
