@@ -26,7 +26,7 @@ EXPORTS = [
     "acmmp_set_params", "acmmp_upload_views", "acmmp_upload_depths", "acmmp_set_state",
     "acmmp_set_scaled_state", "acmmp_set_planar_prior", "acmmp_run_patchmatch", "acmmp_run_patchmatch_ex",
     "acmmp_download", "acmmp_download_aux", "acmmp_device_outputs", "acmmp_synchronize", "acmmp_last_timing",
-    "acmmp_last_kernel_timing", "acmmp_last_work", "acmmp_texel_bytes", "acmmp_jbu",
+    "acmmp_last_kernel_timing", "acmmp_last_work", "acmmp_texel_bytes", "acmmp_set_math", "acmmp_get_math", "acmmp_jbu",
     "acmmp_debug_ncc", "acmmp_debug_geom",
     "acmmp_support_points", "acmmp_delaunay", "acmmp_prior_plane_params", "acmmp_depth_from_plane_param",
     "acmmp_planar_prior_host",
@@ -79,6 +79,8 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_last_kernel_timing.argtypes = [vp, vp, vp]
     L.acmmp_last_work.argtypes = [vp, vp, vp]
     L.acmmp_texel_bytes.argtypes = [vp]
+    L.acmmp_set_math.argtypes = [vp, i32]
+    L.acmmp_get_math.argtypes = [vp]
     L.acmmp_synchronize.argtypes = [vp]
     L.acmmp_jbu.argtypes = [vp, vp, i32, i32, vp, i32, i32, i32, vp]
     L.acmmp_debug_ncc.argtypes = [vp, i32, vp, vp, vp, vp]
@@ -161,6 +163,15 @@ class Context:
         self.close()
 
     # -- setup
+    MATH = {"exact": 0, "fast": 1}
+
+    def set_math(self, mode: str):
+        """'exact' (bit-identical to the oracle, the default) or 'fast' (DESIGN.md §2.4)."""
+        self._check(self.L.acmmp_set_math(self.h, self.MATH[mode]), "set_math")
+
+    def math(self) -> str:
+        return {0: "exact", 1: "fast"}[int(self.L.acmmp_get_math(self.h))]
+
     def set_params(self, params):
         p = np.frombuffer(np.asarray(params, dtype=PARAMS_DTYPE).tobytes(), np.uint8).copy()
         self._params = p

@@ -79,6 +79,7 @@ struct acmmp_ctx {
     unsigned long long* d_work = nullptr;       // [256] k_eval_nb work counters
     unsigned long long work_busy = 0, work_total = 0;
     int klaunch[4] = {0, 0, 0, 0};
+    int math = ACMMP_MATH_EXACT;                // acmmp_set_math
     std::string err;
 };
 
@@ -149,6 +150,14 @@ DevCam acmmp::make_devcam(const acmmp_camera& s) {
     d.Wm1 = s.width - 1; d.Hm1 = s.height - 1;
     d.Hm1f = static_cast<float>(s.height) - 1.0f;
     d.pitch4 = 4 * (s.width + 2);
+    // fast-math constants (float products of the camera's own values)
+    d.fkx = static_cast<float>(s.width) * 0.159154936671257019f;
+    d.fky = static_cast<float>(s.height) * 0.318309873342514038f;
+    for (int r = 0; r < 2; ++r) {
+        for (int k = 0; k < 3; ++k)
+            d.KR[3 * r + k] = std::fmaf(s.K[3 * r + 2], s.R[6 + k], std::fmaf(s.K[3 * r + 1], s.R[3 + k], s.K[3 * r] * s.R[k]));
+        d.Kt[r] = std::fmaf(s.K[3 * r + 2], s.t[2], std::fmaf(s.K[3 * r + 1], s.t[1], s.K[3 * r] * s.t[0]));
+    }
     return d;
 }
 
@@ -189,6 +198,7 @@ acmmp_status acmmp_create(int device, acmmp_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return ACMMP_ERR_HIP;
     acmmp_ctx* c = new acmmp_ctx();
     c->device = device;
+    if (const char* m = std::getenv("ACMMP_MATH")) c->math = (m[0] == 'f') ? ACMMP_MATH_FAST : ACMMP_MATH_EXACT;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return ACMMP_ERR_HIP;
@@ -221,6 +231,15 @@ void acmmp_destroy(acmmp_ctx* c) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
+
+acmmp_status acmmp_set_math(acmmp_ctx* c, int mode) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (mode != ACMMP_MATH_EXACT && mode != ACMMP_MATH_FAST) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "unknown math mode");
+    c->math = mode;
+    return ACMMP_OK;
+}
+
+int acmmp_get_math(const acmmp_ctx* c) { return c ? c->math : -1; }
 
 acmmp_status acmmp_set_params(acmmp_ctx* c, const acmmp_params* p) {
     if (!c || !p) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
@@ -548,6 +567,7 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.cams = c->d_cams;
     kp.img = c->d_img;
     kp.tex16 = c->d_img16 != nullptr;
+    kp.fast = c->math == ACMMP_MATH_FAST;
     kp.dep = c->d_dep;
     kp.dirs = c->d_dirs;
     kp.sph_row = c->d_sph_row;

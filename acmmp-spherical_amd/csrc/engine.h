@@ -50,6 +50,9 @@ struct DevCam {
     const uint16_t* img16_base;
     int img16_bytes;
     int pitch2;                     // bytes per padded binary16 row
+    // fast-math projection constants (KParams::fast)
+    float fkx, fky;                 // SPHERE: W / (2 pi), H / pi
+    float KR[6], Kt[2];             // PINHOLE: rows 0-1 of K * R and K * t
 };
 
 // Per-pixel state handed from k_select to k_eval_ref / k_finish (80 bytes).
@@ -67,6 +70,7 @@ struct PixState {
 struct KParams {
     int model;                      // kPinhole / kSphere, uniform over all views
     int tex16;                      // 1: NCC fetches read the binary16 images (DevCam::img16_base)
+    int fast;                       // 1: fast-math NCC sample projection (acmmp_set_math)
     int W, H, Wh, N, V;             // ref size, colour row width ceil(W/2), images, source views
     int R, inc, nside, S;           // patch radius, radius_increment, offsets per axis, samples
     int rows;                       // rows the reference's checkerboard grid covers

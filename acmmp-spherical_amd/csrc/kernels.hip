@@ -231,6 +231,70 @@ __device__ __forceinline__ float depth_from_plane(float4 ph, float4 d) {
     return (fabsf(denom) < 1e-6f) ? 1e6f : (-ph.w / denom);
 }
 
+// ------------------------------------------------------------------ fast-math sample projection
+//
+// KParams::fast (acmmp_set_math): the per-sample arithmetic of ComputeBilateralNCC
+// (ACMMP.cu:456-476) as the reference's --use_fast_math build (CMakeLists.txt:42) treats it --
+// hardware v_rsq / v_sqrt / v_rcp (<= 1 ulp) instead of the IEEE division and square-root
+// sequences, the translation folded into the rotation's fma chain, W / 2pi and H / pi folded into
+// one constant, and the asin / atan2 polynomials without their special-argument paths (a point on
+// the source camera's vertical axis, tx = tz = 0, has no defined longitude; the reference's atan2f
+// returns 0 there, this returns NaN and the sample's cost is 2.0).  Not bit-identical to the
+// oracle: parity is the tolerance of SURVEY.md §8c (tests/test_gpu_fastmath.py).
+
+// atan(t) on [0, 1]: t + t^3 P(t^2), 7-term minimax, max |error| 1.1e-7 rad
+__device__ __forceinline__ float atan_core_fast(float t) {
+    const float z = t * t;
+    float p = -0.004355291370302439f;
+    p = fmaf(p, z, 0.023039722815155983f);
+    p = fmaf(p, z, -0.05777300149202347f);
+    p = fmaf(p, z, 0.09794192016124725f);
+    p = fmaf(p, z, -0.139765664935112f);
+    p = fmaf(p, z, 0.19962701201438904f);
+    p = fmaf(p, z, -0.3333165943622589f);
+    return fmaf(t * z, p, t);
+}
+
+template <int MODEL, typename Cam>
+__device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float& oy) {
+    if (MODEL == kSphere) {
+        const float tx = fmaf(c.R[2], P.z, fmaf(c.R[1], P.y, fmaf(c.R[0], P.x, c.t[0])));
+        const float ty = fmaf(c.R[5], P.z, fmaf(c.R[4], P.y, fmaf(c.R[3], P.x, c.t[1])));
+        const float tz = fmaf(c.R[8], P.z, fmaf(c.R[7], P.y, fmaf(c.R[6], P.x, c.t[2])));
+        const float r2 = fmaf(tz, tz, fmaf(ty, ty, tx * tx));
+        // -latitude = asin(ty / |t|) (ProjectonCamera_cu :626-630)
+        const float s = __builtin_amdgcn_fmed3f(ty * __builtin_amdgcn_rsqf(r2), -1.0f, 1.0f);
+        const float a = fabsf(s);
+        const bool small = a <= 0.5f;
+        const float zl = fmaf(-0.5f, a, 0.5f);
+        const float cz = det_asin_core(small ? a : __builtin_amdgcn_sqrtf(zl), small ? a * a : zl);
+        const float neg_lat = copysignf(small ? cz : fmaf(-2.0f, cz, kPio2Hi), s);
+        // longitude = atan2(tx, tz) (:631)
+        const float ay = fabsf(tx), ax = fabsf(tz);
+        float r = atan_core_fast(fminf(ax, ay) * __builtin_amdgcn_rcpf(fmaxf(ax, ay)));
+        r = ay > ax ? kPio2Hi - r : r;
+        r = __builtin_bit_cast(int, tz) < 0 ? kPiHi - r : r;
+        const float lon = copysignf(r, tx);
+        ox = fmaf(lon, c.fkx, c.cx);
+        oy = fmaf(neg_lat, c.fky, c.cy);
+        if (r2 < 1e-12f) { ox = c.cx; oy = c.cy; }            // |t| < 1e-6 (:618-622)
+    } else {
+        // K (R P + t) = (K R) P + K t, rows 0-1; the perspective divide by z = R[6..8] P + t[2]
+        const float hx = fmaf(c.KR[2], P.z, fmaf(c.KR[1], P.y, fmaf(c.KR[0], P.x, c.Kt[0])));
+        const float hy = fmaf(c.KR[5], P.z, fmaf(c.KR[4], P.y, fmaf(c.KR[3], P.x, c.Kt[1])));
+        const float tz = fmaf(c.R[8], P.z, fmaf(c.R[7], P.y, fmaf(c.R[6], P.x, c.t[2])));
+        const float inv = __builtin_amdgcn_rcpf(tz);
+        ox = hx * inv;
+        oy = hy * inv;
+    }
+}
+
+// ComputeDepthfromPlaneHypothesis with the hardware reciprocal
+__device__ __forceinline__ float depth_from_plane_fast(float4 ph, float4 d) {
+    const float denom = dot3(ph.x, ph.y, ph.z, d.x, d.y, d.z);
+    return (fabsf(denom) < 1e-6f) ? 1e6f : (-ph.w * __builtin_amdgcn_rcpf(denom));
+}
+
 // GetDistance2Origin, ACMMP.cu:168-173
 __device__ __forceinline__ float dist_to_origin(float4 d, float depth, float4 n) {
     return -dot3(n.x, n.y, n.z, d.x * depth, d.y * depth, d.z * depth);
@@ -465,7 +529,7 @@ constexpr int kPipeG16 = ACMMP_PIPEG16;
 #define ACMMP_RC_CONST_PIPE 0               // 1: PIPE callers (k_eval_ref) also read the reference camera per sample (A/B r01_v27: -3%)
 #endif
 
-template <int MODEL, int VB, int STAGED, bool PIPE, int TEX>
+template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM = 0>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv, float (&cost)[VB]) {
     // SPHERE: the weight sum of every view is the pixel's patch sum (hypothesis- and view-independent);
@@ -488,7 +552,8 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     ConstCam* ccams = (ConstCam*)(kp.cams);
 #define PCV(v) ccams[cv[v]]
     const float4 dc = ray_at<MODEL>(kp, px, py);
-    const float3 Pc3 = world_point_ray<MODEL>(rc, px, py, depth_from_plane(ph, dc), dc);
+    const float3 Pc3 = world_point_ray<MODEL>(rc, px, py, FM ? depth_from_plane_fast(ph, dc) : depth_from_plane(ph, dc),
+                                              dc);
 #pragma unroll
     for (int v = 0; v < VB; ++v) {
         sbw[v] = pt.sbw; sref[v] = pt.sref; srr[v] = pt.srr;
@@ -496,7 +561,8 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
         cval[v] = true;
         if (MODEL == kPinhole && v < nv) {
             float ox, oy, od;
-            project<MODEL>(PCV(v), Pc3, ox, oy, od);
+            if (FM) project_fast<MODEL>(PCV(v), Pc3, ox, oy);
+            else project<MODEL>(PCV(v), Pc3, ox, oy, od);
             cval[v] = !(ox < 0.0f || ox >= PCV(v).Wf || oy < 0.0f || oy >= PCV(v).Hf);
         }
     }
@@ -532,10 +598,11 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             // reference camera through the constant address space too: scalar loads per sample
             // instead of 12 wave-uniform VGPRs held across the loop
             float3 P;
+            const float dep = FM ? depth_from_plane_fast(ph, rw) : depth_from_plane(ph, rw);
             if (!PIPE || ACMMP_RC_CONST_PIPE)
-                P = world_point_ray<MODEL>(ccams[0], px + i, py + j, depth_from_plane(ph, rw), rw);
+                P = world_point_ray<MODEL>(ccams[0], px + i, py + j, dep, rw);
             else
-                P = world_point_ray<MODEL>(rc, px + i, py + j, depth_from_plane(ph, rw), rw);
+                P = world_point_ray<MODEL>(rc, px + i, py + j, dep, rw);
             const float wr = w * r;
             Tap tap[VB];
             bool ok[VB];
@@ -561,11 +628,12 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 if (v < nv) {
                     ConstCam& c = PCV(v);
                     float sx, sy, sd;
-                    project<MODEL>(c, P, sx, sy, sd);
+                    if (FM) project_fast<MODEL>(c, P, sx, sy);
+                    else project<MODEL>(c, P, sx, sy, sd);
                     ok[v] = true;
                     if (MODEL == kSphere) {
                         sx = fmaf(-floorf(sx * c.invW), c.Wf, sx);
-                        sy = clamp0(sy, c.Hm1f);
+                        sy = FM ? __builtin_amdgcn_fmed3f(sy, 0.0f, c.Hm1f) : clamp0(sy, c.Hm1f);
                     } else {
                         ok[v] = !(sx < 0.0f || sx >= c.Wf || sy < 0.0f || sy >= c.Hf);
                     }
@@ -690,7 +758,7 @@ __device__ __forceinline__ float4 perturbed_normal(float4 v, float4 n, Rng& rs, 
 // ------------------------------------------------------------------ cost-vector helpers
 
 // Evaluate all source views of plane `ph` and hand each cost to f(view0, cost) in view order.
-template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, typename F>
+template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM, typename F>
 __device__ __forceinline__ void for_all_views_t(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                                 uint32_t wave_mask, F&& f) {
     int v = 0;
@@ -712,7 +780,7 @@ __device__ __forceinline__ void for_all_views_t(const KParams& kp, int px, int p
         }
         if (nv == 0) break;
         float cost[VB];
-        ncc_chunk<MODEL, VB, STAGED, PIPE, TEX>(kp, px, py, pt, ph, vlist, nv, cost);
+        ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM>(kp, px, py, pt, ph, vlist, nv, cost);
 #pragma unroll
         for (int k = 0; k < VB; ++k)
             if (k < nv) f(vlist[k] - 1, cost[k]);
@@ -720,12 +788,18 @@ __device__ __forceinline__ void for_all_views_t(const KParams& kp, int px, int p
     }
 }
 
-// The same over the binary16 images when the context has them (launch-uniform branch).
-template <int MODEL, int VB, int STAGED, bool PIPE, typename F>
+// The same over the binary16 images when the context has them, with the fast-math projection when
+// the context asks for it (launch-uniform branches).
+template <int MODEL, int VB, int STAGED, bool PIPE, bool PIPE_FM = PIPE, typename F>
 __device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                               uint32_t wave_mask, F&& f) {
-    if (kp.tex16) for_all_views_t<MODEL, VB, STAGED, PIPE, 1>(kp, px, py, pt, ph, wave_mask, f);
-    else for_all_views_t<MODEL, VB, STAGED, PIPE, 0>(kp, px, py, pt, ph, wave_mask, f);
+    if (kp.fast) {
+        if (kp.tex16) for_all_views_t<MODEL, VB, STAGED, PIPE_FM, 1, 1>(kp, px, py, pt, ph, wave_mask, f);
+        else for_all_views_t<MODEL, VB, STAGED, PIPE_FM, 0, 1>(kp, px, py, pt, ph, wave_mask, f);
+    } else {
+        if (kp.tex16) for_all_views_t<MODEL, VB, STAGED, PIPE, 1, 0>(kp, px, py, pt, ph, wave_mask, f);
+        else for_all_views_t<MODEL, VB, STAGED, PIPE, 0, 0>(kp, px, py, pt, ph, wave_mask, f);
+    }
 }
 
 __device__ __forceinline__ float vw_get(const uint32_t (&vwp)[4], int v) {
@@ -1155,6 +1229,10 @@ constexpr int kEvalVB = ACMMP_EVAL_VB;
 #ifndef ACMMP_NB_PIPE
 #define ACMMP_NB_PIPE false                 // experiment switch: all views' texels in flight in k_eval_nb
 #endif
+#ifndef ACMMP_NB_PIPE_FAST
+#define ACMMP_NB_PIPE_FAST true             // the same in fast-math mode, whose shorter projection leaves the
+                                            // registers for it (r02 A/B: k_eval_nb 2.19 -> 2.06 ms; exact -4%)
+#endif
 constexpr int kNbLanes = 8;                 // the 8 neighbour directions (the current plane's costs are cached)
 constexpr int kNbPix = 32;                  // pixels per 256-lane block
 
@@ -1286,7 +1364,8 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? ACMMP_NB_WAVES : 1) void k_
     const float4 ph = plane_at(kp, pos);
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
-    for_all_views<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, ACMMP_NB_PIPE>(kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
+    for_all_views<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, ACMMP_NB_PIPE, ACMMP_NB_PIPE_FAST>(
+        kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
 }
 
 // Joint view selection, aggregation, acceptance and refinement candidates (ACMMP.cu:1146-1311,

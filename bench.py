@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--model", choices=["sphere", "pinhole"], default="sphere")
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--math", choices=["exact", "fast"], default="exact",
+                    help="engine arithmetic (acmmp_set_math): exact = bit-identical to the oracle")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 -> every host core this process may use (affinity and cgroup quota)")
@@ -223,6 +225,7 @@ def main():
     # one GPU per rank; more ranks than GPUs (rehearsal on a small box) share them round-robin
     ndev = capi.device_count()
     ctx = capi.Context(local_rank % ndev if ndev else local_rank)
+    ctx.set_math(args.math)
     ctx.set_params(params)
     ctx.upload_views(sc.images, sc.cameras)
 

@@ -94,6 +94,17 @@ int acmmp_abi_version(void);
 /* Number of visible HIP devices (0 without a GPU); never fails. */
 int acmmp_device_count(void);
 
+/* Arithmetic of the NCC's per-sample projection (ComputeBilateralNCC, ACMMP.cu:456-476).
+ * ACMMP_MATH_EXACT (default): the fixed IEEE definitions of DESIGN.md §2.3 -- results are
+ * bit-identical to the CPU oracle.  ACMMP_MATH_FAST: what the reference's --use_fast_math build
+ * (CMakeLists.txt:42) does to the same arithmetic -- hardware rsq/sqrt/rcp (<= 1 ulp), the
+ * translation folded into the rotation, the asin/atan2 polynomials without special-argument paths
+ * (DESIGN.md §2.4); results within SURVEY.md §8c's tolerances, not bit-identical.  The environment
+ * variable ACMMP_MATH=fast sets the default of new contexts.  No reference counterpart. */
+enum { ACMMP_MATH_EXACT = 0, ACMMP_MATH_FAST = 1 };
+acmmp_status acmmp_set_math(acmmp_ctx *ctx, int mode);
+int acmmp_get_math(const acmmp_ctx *ctx);
+
 /* The params member + Set{GeomConsistency,Hierarchy,PlanarPrior}Params
  * (ACMMP.cpp:548-565).  Copied; may be called again between runs. */
 acmmp_status acmmp_set_params(acmmp_ctx *ctx, const acmmp_params *params);

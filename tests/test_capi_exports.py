@@ -56,7 +56,7 @@ int main(void) {{
     assert vals == [cam.itemsize, par.itemsize, cam.fields["R"][1], cam.fields["width"][1],
                     cam.fields["depth_max"][1], par.fields["scaled_cols"][1],
                     par.fields["geom_consistency"][1], par.fields["upsample"][1]]
-    assert vals[:2] == [120, 68]          # main.h:189-203, ACMMP.h:32-55
+    assert vals[:2] == [120, 68]          # main.h:40-54, ACMMP.h:32-55
 
 
 def test_no_device_fails_loudly():
