@@ -305,7 +305,7 @@ class Pipeline:
     def __init__(self, ds: Dataset, engine=None, exchange=None, device: int = 0, seed: int = 1234,
                  order: str = "reference", geom_iterations: int = 2, out_folder: str | None = None,
                  use_device_store: bool | None = None, size_bound: int = 1000, max_image_size: int = 3200,
-                 log=None, reuse_planes: bool = True):
+                 log=None, reuse_planes: bool = True, math: str | None = None):
         self.ds = ds
         # a geom pass restarts from the previous pass's depth + normals of its view, which is that
         # pass's downloaded plane array: keep it instead of re-joining the two stored maps
@@ -321,6 +321,8 @@ class Pipeline:
         self.device = device
         self.engine = engine if engine is not None else capi.Context(device)
         gpu = isinstance(self.engine, capi.Context)
+        if math is not None and gpu:
+            self.engine.set_math(math)                      # 'exact' (bit-identical) or 'fast' 
         self.store = ViewStore(device if (gpu if use_device_store is None else use_device_store) else None)
         self.seed = seed
         self.geom_iterations = geom_iterations
@@ -660,6 +662,8 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--order", choices=["reference", "snapshot"], default=None)
     ap.add_argument("--geom-iterations", type=int, default=2)
+    ap.add_argument("--math", choices=["exact", "fast"], default=None,
+                    help="engine arithmetic (default: exact, or ACMMP_MATH from the environment)")
     ap.add_argument("--no-dmb", action="store_true", help="keep results in memory only")
     ap.add_argument("--no-fusion", action="store_true", help="skip RunFusionCuda")
     a = ap.parse_args(argv)
@@ -671,7 +675,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     pipe = Pipeline(ds, exchange=exchange, device=device, seed=a.seed, order=order,
                     geom_iterations=a.geom_iterations, out_folder=None if a.no_dmb else a.dense_folder,
-                    log=lambda *m: print(*m, flush=True)).run()
+                    log=lambda *m: print(*m, flush=True), math=a.math).run()
     n_points = None
     if not a.no_fusion:
         pts = pipe.run_fusion(ply_path=os.path.join(a.dense_folder, "ACMMP", "ACMM_model_cuda_5.ply"))

@@ -334,11 +334,20 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
     // ACMMP_TEX16=0 in the environment keeps the fp32 fetches (A/B switch; identical results).
     const char* tex16_env = std::getenv("ACMMP_TEX16");
     if (!(tex16_env && tex16_env[0] == '0')) {
-        HIP_TRY(c, dreserve(c->d_img16, c->img16_cap, static_cast<size_t>(total)));
+        // ACMMP_TEX_PAIRS builds keep the row-pair layout: 4 bytes per texel position, the same offsets
+        // as the fp32 images
+        const bool pairs = tex_pairs_layout() != 0;
+        HIP_TRY(c, dreserve(c->d_img16, c->img16_cap, static_cast<size_t>(total) * (pairs ? 2 : 1)));
         if (!c->d_flag) HIP_TRY(c, dalloc(c->d_flag, 1));
         int inexact = 0;
         HIP_TRY(c, hipMemsetAsync(c->d_flag, 0, sizeof(int), c->stream));
-        HIP_TRY(c, launch_to_f16(c->d_img, total, c->d_img16, c->d_flag, c->stream));
+        if (pairs) {
+            for (int i = 0; i < n; ++i)
+                HIP_TRY(c, launch_to_f16_pairs(c->d_img + off[i], cams[i].width, cams[i].height,
+                                               reinterpret_cast<uint32_t*>(c->d_img16) + off[i], c->d_flag, c->stream));
+        } else {
+            HIP_TRY(c, launch_to_f16(c->d_img, total, c->d_img16, c->d_flag, c->stream));
+        }
         HIP_TRY(c, hipMemcpyAsync(&inexact, c->d_flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         if (inexact) { dfree(c->d_img16); c->img16_cap = 0; }
@@ -356,8 +365,9 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
         d.img_off = off[i];
         d.img_base = c->d_img + off[i];
         d.img_bytes = static_cast<int>(4LL * (s.width + 2) * (s.height + 2));
-        d.img16_base = c->d_img16 ? c->d_img16 + off[i] : nullptr;
-        d.img16_bytes = static_cast<int>(2LL * (s.width + 2) * (s.height + 2));
+        const int tp = tex_pairs_layout() ? 2 : 1;
+        d.img16_base = c->d_img16 ? c->d_img16 + tp * off[i] : nullptr;
+        d.img16_bytes = static_cast<int>(2LL * tp * (s.width + 2) * (s.height + 2));
         d.pitch2 = 2 * (s.width + 2);
         d.dep_off = 0; d.dep_w = 1; d.dep_h = 1;
     }

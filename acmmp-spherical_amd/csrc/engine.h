@@ -162,6 +162,9 @@ hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, cons
 // Padded fp32 images -> binary16 copy; *inexact (device int, pre-zeroed) is set when a texel is not
 // exactly representable as a normal binary16 number or zero.
 hipError_t launch_to_f16(const float* src, long long n, uint16_t* dst, int* inexact, hipStream_t s);
+// Row-pair binary16 copy of one padded view (W + 2) x (H + 2) (kernels.hip ACMMP_TEX_PAIRS layout).
+hipError_t launch_to_f16_pairs(const float* src, int W, int H, uint32_t* dst, int* inexact, hipStream_t s);
+int tex_pairs_layout();
 hipError_t launch_pad_image(const float* src, size_t pitch_floats, int W, int H, float* dst, int dst_pitch,
                             hipStream_t s);
 

@@ -67,8 +67,10 @@ def parse():
     ap.add_argument("--model", choices=["sphere", "pinhole"], default="sphere")
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--seed", type=int, default=1234)
-    ap.add_argument("--math", choices=["exact", "fast"], default="exact",
-                    help="engine arithmetic (acmmp_set_math): exact = bit-identical to the oracle")
+    ap.add_argument("--math", choices=["exact", "fast"], default="fast",
+                    help="engine arithmetic (acmmp_set_math): fast = the reference's --use_fast_math arithmetic "
+                         "(tolerance parity, tests/test_gpu_fastmath.py); exact = bit-identical to the oracle")
+    ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other math mode beside `value`")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 -> every host core this process may use (affinity and cgroup quota)")
@@ -100,7 +102,8 @@ def end_to_end(args, sc, device):
         pr = io.Problem(i)
         pr.src_image_ids = [j for j in range(n) if j != i]
         problems.append(pr)
-    pipe = pipeline.Pipeline(pipeline.Dataset(images, cams, problems), device=device, order="reference")
+    pipe = pipeline.Pipeline(pipeline.Dataset(images, cams, problems), device=device, order="reference",
+                             math=args.math)
     t0 = time.perf_counter()
     pipe.run()
     total = time.perf_counter() - t0
@@ -110,6 +113,7 @@ def end_to_end(args, sc, device):
     return {"views": n, "passes": [p.name for p in pipe.passes], "total_s": round(total, 3),
             "ms_per_view": round(total / n * 1e3, 1),
             "ms_per_view_pass": round(total / (n * len(pipe.passes)) * 1e3, 1),
+            "math": args.math,
             "stages_s": {k: round(v, 3) for k, v in sorted(pipe.stage_s.items())},
             "frac_within_1pct_gt": None if acc is None else round(float(acc), 4),
             "note": "host wall clock, one GPU; every view's final depth map after all passes"}
@@ -254,6 +258,25 @@ def main():
     elapsed = time.perf_counter() - t0
     t_max = allmax(elapsed)
 
+    # the other math mode on the same resident inputs (reported beside `value`, never `value`)
+    other = None
+    if not args.no_other_mode:
+        om = "exact" if args.math == "fast" else "fast"
+        ctx.set_math(om)
+        ctx.run_patchmatch(args.seed + 500)
+        ctx.synchronize()
+        barrier()
+        t_o = time.perf_counter()
+        for k in range(args.steps):
+            ctx.run_patchmatch(args.seed + k)
+        ctx.synchronize()
+        barrier()
+        el_o = allmax(time.perf_counter() - t_o)
+        other = {"math": om, "value": round(args.width * args.height * args.iters * args.steps * world / el_o / 1e6, 3),
+                 "ms_per_step": round(el_o / args.steps * 1e3, 3),
+                 "note": "exact = bit-identical to the CPU oracle; fast = tolerance parity (DESIGN.md §2.4)"}
+        ctx.set_math(args.math)
+
     planes, costs = ctx.download()
     # per-map latency as the reference's RunPatchMatch ends (ACMMP.cu:1553-1554): run + D2H of planes
     # and costs into caller-owned host buffers (inputs resident, as for `value`)
@@ -299,7 +322,7 @@ def main():
         try:
             pm = json.load(open(args.pmc))
             if pm.get("config") == {"width": args.width, "height": args.height, "n_src": args.n_src,
-                                    "model": args.model}:
+                                    "model": args.model, "math": args.math}:
                 traffic = pm.get("kernels", {}).get("k_eval_nb", {}).get("hbm_bytes_per_launch")
                 if traffic:
                     gbs = traffic / (launch_ms * 1e-3) / 1e9
@@ -356,6 +379,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "math": args.math,
+            "other_math_mode": other,
             "data": f"synthetic (ray-cast textured box room, {args.model.upper()} cameras; no dataset reachable)",
             "config": {"workload": f"RunPatchMatch {args.width}x{args.height} {args.model}, 1 ref + {args.n_src} src, "
                                    f"{args.iters} iterations, random init, per-GPU reference view",

@@ -51,6 +51,7 @@ if __name__ == "__main__":
     ap.add_argument("--height", type=int, default=1500)
     ap.add_argument("--n-src", type=int, default=4)
     ap.add_argument("--model", default="sphere")
+    ap.add_argument("--math", default="fast")
     a = ap.parse_args()
     s = summarize(a.root)
     for k, v in sorted(s.items()):
@@ -68,6 +69,6 @@ if __name__ == "__main__":
                           "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "TCC_HIT", "TCC_MISS"):
                     if c in v:
                         kernels[k][c] = v[c]
-        json.dump({"config": {"width": a.width, "height": a.height, "n_src": a.n_src, "model": a.model},
+        json.dump({"config": {"width": a.width, "height": a.height, "n_src": a.n_src, "model": a.model, "math": a.math},
                    "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 bytes per dispatch (gfx950 FETCH_SIZE counts 1/2)",
                    "kernels": kernels}, open(a.json, "w"), indent=1)
