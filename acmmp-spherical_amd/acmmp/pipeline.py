@@ -186,12 +186,23 @@ def fusion_inputs(ds: "Dataset", store, problems):
     return np.array(cams, dtype=types.CAMERA_DTYPE), depths, normals, colours
 
 
+def cpp_round(x) -> int:
+    """std::round of a non-negative float: half away from zero (np.round rounds half to even)."""
+    return int(math.floor(float(x) + 0.5))
+
+
+def round_dims(rows: int, cols: int, size: int):
+    """std::round(rows * factor), std::round(cols * factor) with the float32 factor
+    min(size / cols, size / rows) (ACMMP.cpp:616-621, main.cpp:227-231)."""
+    factor = min(np.float32(size) / np.float32(cols), np.float32(size) / np.float32(rows))
+    return cpp_round(np.float32(rows) * factor), cpp_round(np.float32(cols) * factor)
+
+
 def scaled_dims(rows: int, cols: int, max_image_size: int):
     """(rows, cols) after InuputInitialization's rescale (ACMMP.cpp:607-617): float32 factor, rounded."""
     if cols <= max_image_size and rows <= max_image_size:
         return rows, cols
-    factor = min(np.float32(max_image_size) / np.float32(cols), np.float32(max_image_size) / np.float32(rows))
-    return int(np.round(np.float32(rows) * factor)), int(np.round(np.float32(cols) * factor))
+    return round_dims(rows, cols, max_image_size)
 
 
 def scale_view(image: np.ndarray, cam: np.ndarray, max_image_size: int):
@@ -583,9 +594,7 @@ class Pipeline:
         coarse = self.store.get("depths_geom", ref)
         img = self.ds.images[ref]
         rows, cols = img.shape
-        factor = min(np.float32(acmmp_size) / np.float32(cols), np.float32(acmmp_size) / np.float32(rows))
-        new_cols = int(np.round(np.float32(cols) * factor))
-        new_rows = int(np.round(np.float32(rows) * factor))
+        new_rows, new_cols = round_dims(rows, cols, acmmp_size)
         scaled = resize_linear(img, new_cols, new_rows)
         imagescale = max(scaled.shape[0] // coarse.shape[0], scaled.shape[1] // coarse.shape[1])
         if imagescale == 1:                                          # ACMMP.cpp:1076-1079
@@ -662,6 +671,7 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--order", choices=["reference", "snapshot"], default=None)
     ap.add_argument("--geom-iterations", type=int, default=2)
+    ap.add_argument("--size-bound", type=int, default=1000, help="coarsest-scale bound (main.cpp:38)")
     ap.add_argument("--math", choices=["exact", "fast"], default=None,
                     help="engine arithmetic (default: exact, or ACMMP_MATH from the environment)")
     ap.add_argument("--no-dmb", action="store_true", help="keep results in memory only")
@@ -675,6 +685,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     pipe = Pipeline(ds, exchange=exchange, device=device, seed=a.seed, order=order,
                     geom_iterations=a.geom_iterations, out_folder=None if a.no_dmb else a.dense_folder,
+                    size_bound=a.size_bound,
                     log=lambda *m: print(*m, flush=True), math=a.math).run()
     n_points = None
     if not a.no_fusion:

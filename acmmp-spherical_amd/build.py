@@ -74,5 +74,35 @@ def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines=(),
     return lib
 
 
+HOST = os.path.join(HERE, "host")
+HOST_LIB = os.path.join(HERE, "acmmp", "libacmmp_host.so")
+HOST_EXE = os.path.join(HERE, "acmmp", "ACMMP")
+HOST_SOURCES = ["formats.cpp", "jpeg.cpp"]
+HOST_HEADERS = ["formats.hpp", "jpeg.hpp", "ACMMP.hpp"]
+HOST_FLAGS = ["-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wextra", "-Werror", f"-I{INCLUDE}"]
+
+
+def build_host(force: bool = False, verbose: bool = True, engine_lib: str = LIB):
+    """The C++ host side (plain g++, no GPU code): libacmmp_host.so (formats + JPEG decoder + their
+    test entry points) and the drop-in driver executable `ACMMP` (host/acmmp_main.cpp, the reference's
+    main.cpp) linked against libacmmp.so."""
+    deps = [os.path.join(HOST, f) for f in HOST_SOURCES + HOST_HEADERS + ["host_capi.cpp", "acmmp_main.cpp"]] + \
+        [os.path.join(INCLUDE, "acmmp.h")]
+    outs = [HOST_LIB, HOST_EXE]
+    if not force and all(os.path.exists(o) for o in outs) and min(os.path.getmtime(o) for o in outs) >= _newest(deps):
+        return HOST_LIB, HOST_EXE
+    srcs = [os.path.join(HOST, f) for f in HOST_SOURCES]
+    libdir = os.path.dirname(engine_lib)
+    cmds = [["g++", *HOST_FLAGS, "-shared", "-fPIC", "-o", HOST_LIB, *srcs, os.path.join(HOST, "host_capi.cpp")],
+            ["g++", *HOST_FLAGS, "-o", HOST_EXE, os.path.join(HOST, "acmmp_main.cpp"), *srcs,
+             f"-L{libdir}", "-l:" + os.path.basename(engine_lib), f"-Wl,-rpath,{libdir}"]]
+    for cmd in cmds:
+        if verbose:
+            print("[acmmp build]", " ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return HOST_LIB, HOST_EXE
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_host(force="--force" in sys.argv)

@@ -73,24 +73,3 @@ def test_default_params_match_reference():
     assert (int(p["max_iterations"]), int(p["patch_size"]), int(p["radius_increment"]), int(p["top_k"])) == (3, 11, 2, 4)
     assert float(p["sigma_spatial"]) == 5.0 and float(p["sigma_color"]) == 3.0
     assert np.float32(p["baseline"]) == np.float32(0.54)
-
-
-def build_facade_example(tmp_path):
-    """Compile the C++ facade example (acmmp-spherical_amd/host) against libacmmp.so."""
-    src = os.path.join(REPO, "acmmp-spherical_amd", "host", "process_problem_example.cpp")
-    libdir = os.path.dirname(capi.LIB_PATH)
-    exe = tmp_path / "process_problem_example"
-    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(REPO, "include"),
-                    "-o", str(exe), src, "-L", libdir, "-lacmmp", f"-Wl,-rpath,{libdir}"], check=True)
-    return exe
-
-
-def test_cpp_facade_builds_and_fails_like_cuda_safe_call(tmp_path):
-    """Without a GPU the facade reports the status and exits with EXIT_FAILURE (ACMMP.cpp:64-72)."""
-    import torch
-    if torch.cuda.device_count() > 0:
-        return
-    exe = build_facade_example(tmp_path)
-    r = subprocess.run([str(exe)], capture_output=True, text=True)
-    assert r.returncode == 1
-    assert "no HIP device" in r.stdout and "ACMMP.hpp" in r.stdout
