@@ -1418,8 +1418,16 @@ __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour
 #ifndef ACMMP_NB_WAVES
 #define ACMMP_NB_WAVES 8                    // k_eval_nb (SPHERE): minimum waves per SIMD the register budget must allow
 #endif
-template <int MODEL, int VB>
-__global__ __launch_bounds__(256, MODEL == kSphere ? ACMMP_NB_WAVES : 1) void k_eval_nb(const KParams kp, const int colour) {
+// TEX (binary16 texels) and FM (fast math) are compile-time here, so each of the four variants gets its
+// own register allocation (a runtime branch between them sized every variant for the largest: 23
+// VGPRs spilled at the 64-VGPR budget; r02 A/B profiles/r02_split_nb_ab.txt: fast 388 -> 394, exact
+// 316.6 -> 320 Mpixel-iterations/s)
+#ifndef ACMMP_NB_WAVES_FM
+#define ACMMP_NB_WAVES_FM 7                 // the fast-math instances: 72 VGPRs, no spills (r02 A/B: 7 waves +0.6% over 8)
+#endif
+template <int MODEL, int VB, int TEX, int FM>
+__global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_WAVES_FM : ACMMP_NB_WAVES) : 1) void k_eval_nb(
+    const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kNbLanes, h = t - lp * kNbLanes;
@@ -1443,7 +1451,7 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? ACMMP_NB_WAVES : 1) void k_
     const float4 ph = plane_at(kp, pos);
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
-    for_all_views<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, ACMMP_NB_PIPE, ACMMP_NB_PIPE_FAST>(
+    for_all_views_t<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, FM ? ACMMP_NB_PIPE_FAST : ACMMP_NB_PIPE, TEX, FM>(
         kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
 }
 
@@ -2208,7 +2216,16 @@ hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut ou
     // roofline prices is that kernel alone
     if (ACMMP_PICK_PASS) k_pick<<<dim3(cdiv(npix, 256), 8), 256, 0, s>>>(kp, colour);
     ACMMP_MARK(0);
-    ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC><<<eval_grid(cdiv(npix, kNbPix)), 256, lds_nb, s>>>(kp, colour)));
+    {
+        const dim3 grd = eval_grid(cdiv(npix, kNbPix));
+        if (kp.fast) {
+            if (kp.tex16) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 1, 1><<<grd, 256, lds_nb, s>>>(kp, colour)));
+            else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 0, 1><<<grd, 256, lds_nb, s>>>(kp, colour)));
+        } else {
+            if (kp.tex16) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 1, 0><<<grd, 256, lds_nb, s>>>(kp, colour)));
+            else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 0, 0><<<grd, 256, lds_nb, s>>>(kp, colour)));
+        }
+    }
     ACMMP_MARK(1);
     if (kp.geom) ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, true><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
     else ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, false><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));

@@ -378,14 +378,3 @@ def test_api_errors(ctx):
         fresh.set_planar_prior(np.zeros((H + 1, W, 4), np.float32), np.zeros((H, W), np.uint32))
     fresh.close()
 
-
-def test_cpp_facade_example_runs(tmp_path):
-    """The C++ ACMMP facade (acmmp-spherical_amd/host) drives the engine like ProcessProblem
-    (main.cpp:83-111): fronto-parallel synthetic scene at depth 5 (mean depth within range)."""
-    from test_capi_exports import build_facade_example
-    import subprocess
-    exe = build_facade_example(tmp_path)
-    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stdout + r.stderr
-    mean = float(r.stdout.split()[2])
-    assert 3.0 * 0.6 <= mean <= 8.0 * 1.2
