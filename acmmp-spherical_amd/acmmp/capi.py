@@ -29,7 +29,7 @@ EXPORTS = [
     "acmmp_last_kernel_timing", "acmmp_last_work", "acmmp_texel_bytes", "acmmp_set_math", "acmmp_get_math", "acmmp_jbu",
     "acmmp_debug_ncc", "acmmp_debug_geom",
     "acmmp_support_points", "acmmp_delaunay", "acmmp_prior_plane_params", "acmmp_depth_from_plane_param",
-    "acmmp_planar_prior_host",
+    "acmmp_planar_prior_host", "acmmp_set_planar_prior_from_maps", "acmmp_download_planar_prior",
     "acmmp_upload_depths_device", "acmmp_upload_views_device", "acmmp_export_depth", "acmmp_device_alloc", "acmmp_device_free", "acmmp_memcpy",
     "acmmp_comm_unique_id", "acmmp_comm_create", "acmmp_comm_destroy", "acmmp_comm_broadcast",
     "acmmp_comm_allreduce_max",
@@ -106,6 +106,8 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_fusion_last_error.argtypes = [vp]
     L.acmmp_fusion_destroy.argtypes = [vp]
     L.acmmp_planar_prior_host.argtypes = [vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]
+    L.acmmp_set_planar_prior_from_maps.argtypes = [vp, vp, vp, C.c_float, C.c_float, vp]
+    L.acmmp_download_planar_prior.argtypes = [vp, vp, vp]
     for name in EXPORTS:
         fn = getattr(L, name)
         if name not in ("acmmp_destroy", "acmmp_status_str", "acmmp_last_error", "acmmp_abi_version", "acmmp_device_count",
@@ -250,6 +252,24 @@ class Context:
         self._check_hw(pr, (4,), "set_planar_prior planes")
         self._check_hw(mk, (), "set_planar_prior masks")
         self._check(self.L.acmmp_set_planar_prior(self.h, _p(pr), _p(mk)), "set_planar_prior")
+
+    def set_planar_prior_from_maps(self, depths, costs, depth_min: float, depth_max: float) -> int:
+        """The planar block of ProcessProblem with its per-pixel work on the device (main.cpp:113-181):
+        the same prior as planar_prior_host + set_planar_prior.  Returns the triangle count."""
+        d = np.ascontiguousarray(depths, np.float32)
+        c = np.ascontiguousarray(costs, np.float32)
+        self._check_hw(d, (), "set_planar_prior_from_maps depths")
+        self._check_hw(c, (), "set_planar_prior_from_maps costs")
+        n = C.c_int(0)
+        self._check(self.L.acmmp_set_planar_prior_from_maps(self.h, _p(d), _p(c), float(depth_min), float(depth_max),
+                                                            C.byref(n)), "set_planar_prior_from_maps")
+        return n.value
+
+    def download_planar_prior(self):
+        prior = np.empty((self.H, self.W, 4), np.float32)
+        masks = np.empty((self.H, self.W), np.uint32)
+        self._check(self.L.acmmp_download_planar_prior(self.h, _p(prior), _p(masks)), "download_planar_prior")
+        return prior, masks
 
     # -- run
     def run_patchmatch(self, seed: int, n_half_sweeps: int = -1, do_post: bool = True):

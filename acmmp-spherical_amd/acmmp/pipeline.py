@@ -488,12 +488,18 @@ class Pipeline:
             planes, costs = e.download()
         if planar:                                                   # main.cpp:113-187
             p["planar_prior"] = 1
-            with self._timed("planar_prior_host"):
-                prior, masks, _ = capi.planar_prior_host(c0, planes[..., 3], costs, float(p["depth_min"]),
-                                                         float(p["depth_max"]))
-            with self._timed("upload"):
-                e.set_params(p)
-                e.set_planar_prior(prior, masks)
+            if hasattr(e, "set_planar_prior_from_maps"):
+                # support points + Delaunay + planes on the host, raster + mask on the device
+                with self._timed("planar_prior"):
+                    e.set_params(p)
+                    e.set_planar_prior_from_maps(planes[..., 3], costs, float(p["depth_min"]), float(p["depth_max"]))
+            else:
+                with self._timed("planar_prior"):
+                    prior, masks, _ = capi.planar_prior_host(c0, planes[..., 3], costs, float(p["depth_min"]),
+                                                             float(p["depth_max"]))
+                with self._timed("upload"):
+                    e.set_params(p)
+                    e.set_planar_prior(prior, masks)
             with self._timed("patchmatch"):
                 e.run_patchmatch(run_seed + 1)
                 planes, costs = e.download()

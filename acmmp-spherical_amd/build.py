@@ -23,8 +23,8 @@ ARCH = os.environ.get("ACMMP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["kernels.hip", "capi.cpp", "comm.cpp", "fusion.cpp", "planar_prior.cpp"]
-HIP_CPP = {"capi.cpp", "comm.cpp", "fusion.cpp"}              # host C++ that includes HIP headers
-HEADERS = ["engine.h", "detmath.h"]
+HIP_CPP = {"capi.cpp", "comm.cpp", "fusion.cpp", "planar_prior.cpp"}              # host C++ that includes HIP headers
+HEADERS = ["engine.h", "detmath.h", "planar.h"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize", f"--offload-arch={ARCH}",
           f"-I{INCLUDE}", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
 

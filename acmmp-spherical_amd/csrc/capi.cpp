@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "planar.h"
 
 using namespace acmmp;
 
@@ -64,7 +65,10 @@ struct acmmp_ctx {
 
     float4* d_prior = nullptr;
     uint32_t* d_mask = nullptr;
+    size_t prior_cap = 0, mask_cap = 0;
     bool has_prior = false;           // set_planar_prior since the last upload_views
+    char* d_pp = nullptr;             // planar-prior triangle tables (acmmp_set_planar_prior_from_maps)
+    size_t pp_cap = 0;
 
     float4* d_plane_cs[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
     float* d_cost_cs[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
@@ -221,7 +225,7 @@ void acmmp_destroy(acmmp_ctx* c) {
     dfree(c->d_stage); dfree(c->d_flag);
     dfree(c->d_sph_row); dfree(c->d_sph_col); dfree(c->d_spatial);
     dfree(c->d_planes_rm); dfree(c->d_costs_rm); dfree(c->d_pre); dfree(c->d_sel_rm);
-    dfree(c->d_scaled); dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_scratch); dfree(c->d_work);
+    dfree(c->d_scaled); dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_pp); dfree(c->d_scratch); dfree(c->d_work);
     for (int k = 0; k < 2; ++k) {
         for (int b = 0; b < 2; ++b) { dfree(c->d_plane_cs[k][b]); dfree(c->d_cost_cs[k][b]); }
         dfree(c->d_sel_cs[k]); dfree(c->d_rng_cs[k]);
@@ -394,6 +398,7 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
             HIP_TRY(c, dalloc(c->d_rng_cs[k], Pc));
         }
         dfree(c->d_prior); dfree(c->d_mask);
+        c->prior_cap = c->mask_cap = 0;
         dfree(c->d_scratch);
         c->scratch_bytes = 0;
     }
@@ -475,11 +480,74 @@ acmmp_status acmmp_set_planar_prior(acmmp_ctx* c, const float* prior, const uint
     if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
     HIP_TRY(c, hipSetDevice(c->device));
     const size_t P = P_of(c);
-    HIP_TRY(c, dalloc(c->d_prior, P));
-    HIP_TRY(c, dalloc(c->d_mask, P));
+    HIP_TRY(c, dreserve(c->d_prior, c->prior_cap, P));
+    HIP_TRY(c, dreserve(c->d_mask, c->mask_cap, P));
     HIP_TRY(c, hipMemcpy(c->d_prior, prior, sizeof(float4) * P, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(c->d_mask, masks, sizeof(uint32_t) * P, hipMemcpyHostToDevice));
     c->has_prior = true;
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_set_planar_prior_from_maps(acmmp_ctx* c, const float* depths, const float* costs, float depth_min,
+                                              float depth_max, int* n_triangles) {
+    if (!c || !depths || !costs) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
+    if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const acmmp_camera& cam = c->cams[0];
+    const int W = c->W, H = c->H;
+    const size_t P = P_of(c);
+    PlanarTriangles pt;
+    const acmmp_status st = planar_triangles(cam, depths, costs, W, H, &pt);
+    if (st != ACMMP_OK) return fail(c, st, "planar_triangles");
+    const int m = static_cast<int>(pt.step.size());
+    // one upload: first[] (8 B aligned) | plane (float4) | tri | step | row/col trig
+    auto up = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
+    const size_t o_first = 0, n_first = sizeof(long long) * (m + 1);
+    const size_t o_plane = up(o_first + n_first), n_plane = sizeof(float) * pt.plane.size();
+    const size_t o_tri = up(o_plane + n_plane), n_tri = sizeof(int) * pt.tri.size();
+    const size_t o_step = up(o_tri + n_tri), n_step = sizeof(float) * pt.step.size();
+    const size_t o_row = up(o_step + n_step), n_row = sizeof(float2) * pt.row_trig.size();
+    const size_t o_col = up(o_row + n_row), n_col = sizeof(float2) * pt.col_trig.size();
+    const size_t bytes = up(o_col + n_col);
+    std::vector<char> host(bytes);
+    std::memcpy(host.data() + o_first, pt.first.data(), n_first);
+    if (n_plane) std::memcpy(host.data() + o_plane, pt.plane.data(), n_plane);
+    if (n_tri) std::memcpy(host.data() + o_tri, pt.tri.data(), n_tri);
+    if (n_step) std::memcpy(host.data() + o_step, pt.step.data(), n_step);
+    if (n_row) std::memcpy(host.data() + o_row, pt.row_trig.data(), n_row);
+    if (n_col) std::memcpy(host.data() + o_col, pt.col_trig.data(), n_col);
+    HIP_TRY(c, dreserve(c->d_pp, c->pp_cap, bytes));
+    HIP_TRY(c, dreserve(c->d_prior, c->prior_cap, P));
+    HIP_TRY(c, dreserve(c->d_mask, c->mask_cap, P));
+    HIP_TRY(c, hipMemcpyAsync(c->d_pp, host.data(), bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_mask, 0, sizeof(uint32_t) * P, c->stream));
+    PlanarDev pd;
+    pd.first = reinterpret_cast<const long long*>(c->d_pp + o_first);
+    pd.plane = reinterpret_cast<const float4*>(c->d_pp + o_plane);
+    pd.tri = reinterpret_cast<const int*>(c->d_pp + o_tri);
+    pd.step = reinterpret_cast<const float*>(c->d_pp + o_step);
+    pd.row_trig = reinterpret_cast<const float2*>(c->d_pp + o_row);
+    pd.col_trig = reinterpret_cast<const float2*>(c->d_pp + o_col);
+    pd.n_tri = m;
+    pd.n_steps = pt.first[m];
+    pd.W = W; pd.H = H; pd.model = cam.model;
+    pd.K0 = cam.K[0]; pd.K2 = cam.K[2]; pd.K4 = cam.K[4]; pd.K5 = cam.K[5];
+    pd.depth_min = depth_min; pd.depth_max = depth_max;
+    HIP_TRY(c, launch_planar_raster(pd, c->d_mask, c->stream));
+    HIP_TRY(c, launch_planar_mask(pd, c->d_mask, c->d_prior, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));       // `host` is pageable and goes out of scope
+    c->has_prior = true;
+    if (n_triangles) *n_triangles = m;
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_download_planar_prior(acmmp_ctx* c, float* prior, uint32_t* masks) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (!c->has_prior) return fail(c, ACMMP_ERR_STATE, "no planar prior set since the last upload_views");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t P = P_of(c);
+    if (prior) HIP_TRY(c, hipMemcpy(prior, c->d_prior, sizeof(float4) * P, hipMemcpyDeviceToHost));
+    if (masks) HIP_TRY(c, hipMemcpy(masks, c->d_mask, sizeof(uint32_t) * P, hipMemcpyDeviceToHost));
     return ACMMP_OK;
 }
 

@@ -20,6 +20,7 @@
 
 #include "detmath.h"
 #include "engine.h"
+#include "planar.h"
 
 namespace acmmp {
 
@@ -2258,6 +2259,81 @@ hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s) {
         k_filter<<<grd, blk, 0, s>>>(kp, 0);
         k_filter<<<grd, blk, 0, s>>>(kp, 1);
     }
+    return hipGetLastError();
+}
+
+
+// ------------------------------------------------------------------ kernels: planar prior (device half)
+//
+// ProcessProblem's triangle rasterisation and prior-depth mask (main.cpp:138-181) with the triangles,
+// planes and steps the host computed (planar.h).  One thread per (triangle, p step): the p values are
+// the reference's running float sums 0, step, 2 step, ... (recomputed by the same additions), the q
+// loop runs as in the reference; the reference overwrites labels in triangle order, so a pixel keeps
+// the largest label that reaches it -- atomicMax gives that whatever the schedule.  Same float and
+// double arithmetic as the reference's C++ (no contraction): the same pixels, bit for bit.
+__global__ __launch_bounds__(256) void k_planar_raster(const PlanarDev pd, uint32_t* mask) {
+    const long long t = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= pd.n_steps) return;
+    int lo = 0, hi = pd.n_tri - 1;                       // triangle k with first[k] <= t < first[k + 1]
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pd.first[mid] <= t) lo = mid;
+        else hi = mid - 1;
+    }
+    const int k = lo;
+    const long long i = t - pd.first[k];
+    const float step = pd.step[k];
+    float p = 0.f;
+    for (long long a = 0; a < i; ++a) p += step;
+    const int* tr = pd.tri + 6 * static_cast<long long>(k);
+    const uint32_t label = static_cast<uint32_t>(k) + 1u;
+    const double rest = 1.0 - static_cast<double>(p);
+    for (float q = 0.f; static_cast<double>(q) < rest; q += step) {
+        const double w3 = rest - static_cast<double>(q);
+        const int x = static_cast<int>(static_cast<double>(p * static_cast<float>(tr[0]) + q * static_cast<float>(tr[2])) +
+                                       w3 * static_cast<double>(tr[4]));
+        const int y = static_cast<int>(static_cast<double>(p * static_cast<float>(tr[1]) + q * static_cast<float>(tr[3])) +
+                                       w3 * static_cast<double>(tr[5]));
+        if (x >= 0 && x < pd.W && y >= 0 && y < pd.H) atomicMax(mask + static_cast<long long>(y) * pd.W + x, label);
+    }
+}
+
+// GetDepthFromPlaneParam (ACMMP.cpp:991-1011) per labelled pixel; out-of-range prior depths drop the
+// label (main.cpp:168-180); CudaPlanarPriorInitialization's expansion (ACMMP.cpp:855-862).
+__global__ __launch_bounds__(256) void k_planar_mask(const PlanarDev pd, uint32_t* mask, float4* prior) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
+    if (i >= pd.W) return;
+    const long long c = static_cast<long long>(j) * pd.W + i;
+    uint32_t l = mask[c];
+    float4 pl = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (l > 0) {
+        pl = pd.plane[l - 1];
+        float d;
+        if (pd.model == kSphere) {
+            const float2 lat = pd.row_trig[j], lon = pd.col_trig[i];
+            const float dx = lat.y * lon.x, dy = -lat.x, dz = lat.y * lon.y;
+            const float denom = pl.x * dx + pl.y * dy + pl.z * dz;
+            d = (fabsf(denom) < 1e-6f) ? 1e6f : (-pl.w / denom);
+        } else {
+            d = -pl.w * pd.K0 / ((static_cast<float>(i) - pd.K2) * pl.x +
+                                 (pd.K0 / pd.K4) * (static_cast<float>(j) - pd.K5) * pl.y + pd.K0 * pl.z);
+        }
+        if (!(d <= pd.depth_max && d >= pd.depth_min)) {
+            l = 0;
+            pl = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    mask[c] = l;
+    prior[c] = pl;
+}
+
+hipError_t launch_planar_raster(const PlanarDev& pd, uint32_t* mask, hipStream_t s) {
+    if (pd.n_steps > 0) k_planar_raster<<<static_cast<unsigned>(cdiv(pd.n_steps, 256)), 256, 0, s>>>(pd, mask);
+    return hipGetLastError();
+}
+
+hipError_t launch_planar_mask(const PlanarDev& pd, uint32_t* mask, float4* prior, hipStream_t s) {
+    k_planar_mask<<<dim3(cdiv(pd.W, 256), pd.H), 256, 0, s>>>(pd, mask, prior);
     return hipGetLastError();
 }
 

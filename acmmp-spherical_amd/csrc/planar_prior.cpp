@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "acmmp.h"
+#include "planar.h"
 
 namespace {
 
@@ -351,42 +352,18 @@ acmmp_status acmmp_planar_prior_host(const acmmp_camera* cam, const float* depth
                                      int* n_triangles) {
     if (!cam || !depths || !costs || !prior_planes || !masks || W <= 0 || H <= 0) return ACMMP_ERR_INVALID_ARGUMENT;
     const size_t P = static_cast<size_t>(W) * H;
-    // GetSupportPoints + DelaunayTriangulation (main.cpp:120-121)
-    const std::vector<int> xy = support_points(costs, W, H);
-    const int n = static_cast<int>(xy.size() / 2);
-    std::vector<int> tri;
-    if (n > 0) {                                           // triangulate once (ACMMP.cpp:932-955)
-        std::vector<Pt> pts(n);
-        for (int i = 0; i < n; ++i) pts[i] = {xy[2 * i], xy[2 * i + 1]};
-        Delaunay dl(pts, std::max<long long>(std::max(W, H), 1));
-        dl.run();
-        for (const auto& t : dl.triangles())
-            for (int j = 0; j < 3; ++j) { tri.push_back(xy[2 * t[j]]); tri.push_back(xy[2 * t[j] + 1]); }
-    }
-    const int m = static_cast<int>(tri.size() / 6);
-    // triangles inside the image get labels 1, 2, ... in order (main.cpp:138-162)
-    std::vector<uint32_t> label_of(m, 0);
-    uint32_t idx = 0;
-    for (int k = 0; k < m; ++k) {
-        const int* t = &tri[6 * static_cast<size_t>(k)];
-        bool inside = true;
-        for (int j = 0; j < 3; ++j) inside = inside && t[2 * j] >= 0 && t[2 * j] < W && t[2 * j + 1] >= 0 && t[2 * j + 1] < H;
-        if (inside) label_of[k] = ++idx;
-    }
+    acmmp::PlanarTriangles pt;
+    const acmmp_status st = acmmp::planar_triangles(*cam, depths, costs, W, H, &pt);
+    if (st != ACMMP_OK) return st;
+    const int m = static_cast<int>(pt.step.size());
     // Rasterise in parallel.  The reference overwrites labels in triangle order, so a pixel ends with
     // the label of the LAST triangle that covered it -- the largest label: an atomic max gives the same
-    // mask whatever the thread schedule.  Per-triangle planes are independent.
+    // mask whatever the thread schedule.
     std::vector<uint32_t> lab(P, 0u);
-    std::vector<float> plane_params(4 * static_cast<size_t>(idx));
     parallel_for(m, [&](int k) {
-        const uint32_t label = label_of[k];
-        if (!label) return;
-        const int* t = &tri[6 * static_cast<size_t>(k)];
-        const float L01 = static_cast<float>(std::sqrt(std::pow(t[0] - t[2], 2) + std::pow(t[1] - t[3], 2)));
-        const float L02 = static_cast<float>(std::sqrt(std::pow(t[0] - t[4], 2) + std::pow(t[1] - t[5], 2)));
-        const float L12 = static_cast<float>(std::sqrt(std::pow(t[2] - t[4], 2) + std::pow(t[3] - t[5], 2)));
-        const float max_edge_length = std::max(L01, std::max(L02, L12));
-        const float step = static_cast<float>(1.0 / max_edge_length);
+        const uint32_t label = static_cast<uint32_t>(k) + 1u;
+        const int* t = &pt.tri[6 * static_cast<size_t>(k)];
+        const float step = pt.step[k];
         for (float p = 0; p < 1.0; p += step) {
             for (float q = 0; q < 1.0 - p; q += step) {
                 const int x = static_cast<int>(static_cast<double>(p * t[0] + q * t[2]) + (1.0 - p - q) * t[4]);
@@ -397,30 +374,88 @@ acmmp_status acmmp_planar_prior_host(const acmmp_camera* cam, const float* depth
                                                                   __ATOMIC_RELAXED)) {}
             }
         }
-        acmmp_prior_plane_params(cam, depths, W, H, t, &plane_params[4 * static_cast<size_t>(label - 1)]);
     });
     // prior depth range check (main.cpp:167-180) and CudaPlanarPriorInitialization (ACMMP.cpp:851-861);
     // every pixel is independent (mask_tri holds float labels idx + 1.0, exact below 2^24)
     const bool sphere = cam->model == ACMMP_SPHERE;
-    std::vector<SphereTrig> lon_of(sphere ? W : 0);
-    for (int i = 0; sphere && i < W; ++i) lon_of[i] = sphere_col(*cam, i);
     parallel_for(H, [&](int j) {
-        const SphereTrig lat = sphere ? sphere_row(*cam, j) : SphereTrig{0.f, 0.f};
+        const SphereTrig lat = sphere ? SphereTrig{pt.row_trig[j].x, pt.row_trig[j].y} : SphereTrig{0.f, 0.f};
         for (int i = 0; i < W; ++i) {
             const size_t c = static_cast<size_t>(j) * W + i;
             uint32_t l = lab[c];
             if (l > 0) {
-                const float* pl = &plane_params[4 * static_cast<size_t>(l - 1)];
-                const float d = sphere ? sphere_depth(pl, lat, lon_of[i]) : acmmp_depth_from_plane_param(cam, pl, i, j);
+                const float* pl = &pt.plane[4 * static_cast<size_t>(l - 1)];
+                const float d = sphere ? sphere_depth(pl, lat, SphereTrig{pt.col_trig[i].x, pt.col_trig[i].y})
+                                       : acmmp_depth_from_plane_param(cam, pl, i, j);
                 if (!(d <= depth_max && d >= depth_min)) l = 0;
             }
             masks[c] = l;
-            if (l > 0) std::memcpy(prior_planes + 4 * c, &plane_params[4 * static_cast<size_t>(l - 1)], 4 * sizeof(float));
+            if (l > 0) std::memcpy(prior_planes + 4 * c, &pt.plane[4 * static_cast<size_t>(l - 1)], 4 * sizeof(float));
             else std::memset(prior_planes + 4 * c, 0, 4 * sizeof(float));
         }
     });
-    if (n_triangles) *n_triangles = static_cast<int>(idx);
+    if (n_triangles) *n_triangles = m;
     return ACMMP_OK;
 }
 
 }  // extern "C"
+
+namespace acmmp {
+
+// Host half of the planar block (planar.h): GetSupportPoints + DelaunayTriangulation, the triangles
+// ProcessProblem labels (main.cpp:138-145: all vertices inside the image, labels 1, 2, ... in
+// triangle order), each one's plane (GetPriorPlaneParams through the first run's depths) and
+// sampling step, the per-triangle count of the p loop (main.cpp:153) as a prefix, and the SPHERE
+// row/column trig tables of GetDepthFromPlaneParam.
+acmmp_status planar_triangles(const acmmp_camera& cam, const float* depths, const float* costs, int W, int H,
+                              PlanarTriangles* out) {
+    const std::vector<int> xy = support_points(costs, W, H);
+    const int n = static_cast<int>(xy.size() / 2);
+    std::vector<int> tri;
+    if (n > 0) {                                           // triangulate once (ACMMP.cpp:932-955)
+        std::vector<Pt> pts(n);
+        for (int i = 0; i < n; ++i) pts[i] = {xy[2 * i], xy[2 * i + 1]};
+        Delaunay dl(pts, std::max<long long>(std::max(W, H), 1));
+        dl.run();
+        for (const auto& t : dl.triangles()) {
+            bool inside = true;
+            for (int j = 0; j < 3; ++j) {
+                const int x = xy[2 * t[j]], y = xy[2 * t[j] + 1];
+                inside = inside && x >= 0 && x < W && y >= 0 && y < H;
+            }
+            if (!inside) continue;
+            for (int j = 0; j < 3; ++j) { tri.push_back(xy[2 * t[j]]); tri.push_back(xy[2 * t[j] + 1]); }
+        }
+    }
+    const int m = static_cast<int>(tri.size() / 6);
+    out->tri = std::move(tri);
+    out->plane.assign(4 * static_cast<size_t>(m), 0.f);
+    out->step.assign(m, 0.f);
+    std::vector<long long> np(m, 0);
+    parallel_for(m, [&](int k) {
+        const int* t = &out->tri[6 * static_cast<size_t>(k)];
+        const float L01 = static_cast<float>(std::sqrt(std::pow(t[0] - t[2], 2) + std::pow(t[1] - t[3], 2)));
+        const float L02 = static_cast<float>(std::sqrt(std::pow(t[0] - t[4], 2) + std::pow(t[1] - t[5], 2)));
+        const float L12 = static_cast<float>(std::sqrt(std::pow(t[2] - t[4], 2) + std::pow(t[3] - t[5], 2)));
+        const float max_edge_length = std::max(L01, std::max(L02, L12));
+        const float step = static_cast<float>(1.0 / max_edge_length);
+        out->step[k] = step;
+        long long c = 0;
+        for (float p = 0; p < 1.0; p += step) ++c;
+        np[k] = c;
+        acmmp_prior_plane_params(&cam, depths, W, H, t, &out->plane[4 * static_cast<size_t>(k)]);
+    });
+    out->first.assign(static_cast<size_t>(m) + 1, 0);
+    for (int k = 0; k < m; ++k) out->first[k + 1] = out->first[k] + np[k];
+    out->row_trig.clear();
+    out->col_trig.clear();
+    if (cam.model == ACMMP_SPHERE) {
+        out->row_trig.resize(H);
+        out->col_trig.resize(W);
+        for (int y = 0; y < H; ++y) { const SphereTrig r = sphere_row(cam, y); out->row_trig[y] = make_float2(r.s, r.c); }
+        for (int x = 0; x < W; ++x) { const SphereTrig k = sphere_col(cam, x); out->col_trig[x] = make_float2(k.s, k.c); }
+    }
+    return ACMMP_OK;
+}
+
+}  // namespace acmmp

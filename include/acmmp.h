@@ -263,6 +263,18 @@ acmmp_status acmmp_planar_prior_host(const acmmp_camera *cam0, const float *dept
                                      int H, float depth_min, float depth_max, float *prior_planes,
                                      uint32_t *masks, int *n_triangles);
 
+/* The same planar block with its per-pixel work on this context's GPU, straight into the context's
+ * planar-prior state: support points, Delaunay and the per-triangle planes on the host (depths/costs:
+ * the first RunPatchMatch's output, W x H of the uploaded reference view), the triangle
+ * rasterisation (main.cpp:153-159), the prior-depth range mask (main.cpp:168-180) and the per-pixel
+ * expansion (ACMMP.cpp:855-862) on the device.  Equivalent to acmmp_planar_prior_host followed by
+ * acmmp_set_planar_prior, bit for bit (tests/test_gpu_parity.py), without the host raster and the
+ * 20 B/pixel upload.  No reference counterpart. */
+acmmp_status acmmp_set_planar_prior_from_maps(acmmp_ctx *ctx, const float *depths, const float *costs,
+                                              float depth_min, float depth_max, int *n_triangles);
+/* Test hook: the planar-prior state of the context (P float4 planes, P labels; either may be NULL). */
+acmmp_status acmmp_download_planar_prior(acmmp_ctx *ctx, float *prior_planes, uint32_t *masks);
+
 /* RunJBU / JBU::CudaRun (ACMMP.cpp:1071-1122, ACMMP.cu:1558-1649): joint bilateral
  * upsampling of `coarse` (sw x sh) guided by `ref` (W x H).  imagescale as the
  * reference computes it: max(H / sh, W / sw) (integer division). */

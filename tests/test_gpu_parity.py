@@ -378,3 +378,33 @@ def test_api_errors(ctx):
         fresh.set_planar_prior(np.zeros((H + 1, W, 4), np.float32), np.zeros((H, W), np.uint32))
     fresh.close()
 
+
+
+@pytest.mark.parametrize("kind,W,H", [("pinhole", 160, 120), ("sphere", 256, 128), ("sphere", 2000, 1500),
+                                      ("pinhole", 1600, 1200)])
+def test_planar_prior_device_equals_host(ctx, kind, W, H):
+    """acmmp_set_planar_prior_from_maps (raster + range mask + expansion on the device) writes exactly
+    the prior planes and labels acmmp_planar_prior_host computes (main.cpp:113-181), on the first
+    run's real depth/cost maps -- including the full-size views with ~10^5 triangles."""
+    sc = (scene.pinhole_scene(W, H, n_src=2, seed=4) if kind == "pinhole" else scene.sphere_scene(W, H, n_src=2, seed=4))
+    p = params_for(sc)
+    r = gpu_run(ctx, sc, p, 21)
+    depths, costs = r["planes"][..., 3].copy(), r["costs"]
+    prior_h, masks_h, n_h = capi.planar_prior_host(sc.cameras[0], depths, costs, float(p["depth_min"]),
+                                                   float(p["depth_max"]))
+    n_d = ctx.set_planar_prior_from_maps(depths, costs, float(p["depth_min"]), float(p["depth_max"]))
+    prior_d, masks_d = ctx.download_planar_prior()
+    assert n_d == n_h and n_h > 0
+    assert np.array_equal(masks_d, masks_h)
+    assert_bitwise_equal(prior_d, prior_h, "prior planes")
+    assert (masks_h > 0).mean() > 0.05
+    # the planar pass then runs from either state identically
+    q = params_for(sc, planar_prior=1)
+    ctx.set_params(q)
+    ctx.run_patchmatch(22)
+    a = ctx.download()
+    ctx.set_planar_prior(prior_h, masks_h)
+    ctx.run_patchmatch(22)
+    b = ctx.download()
+    assert_bitwise_equal(a[0], b[0], "planes after the planar run")
+    assert_bitwise_equal(a[1], b[1], "costs after the planar run")
