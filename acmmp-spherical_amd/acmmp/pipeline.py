@@ -308,6 +308,9 @@ class ViewStore:
 class PassLog:
     name: str
     views: list = field(default_factory=list)
+    compute_s: float = 0.0            # this rank's ProcessProblem calls of the pass (host wall clock)
+    exchange_s: float = 0.0           # the depth-map exchange after it (world > 1)
+    exchange_bytes: int = 0           # depth-map bytes every rank holds after the exchange
 
 
 class Pipeline:
@@ -391,10 +394,12 @@ class Pipeline:
         name = ("geom" + ("_multi" if multi else "")) if geom else ("hier_planar" if hier else "planar")
         self.log(f"[rank {self.rank}] pass {self.pass_index}: {name}")
         log = PassLog(name)
+        t0 = time.perf_counter()
         for i in self.my_problems():
             self.process_problem(i, geom, planar, hier, multi)
             log.views.append(self.problems[i].ref_image_id)
         self._commit_pending()
+        log.compute_s = time.perf_counter() - t0
         key = "depths_geom" if geom else "depths"
         if self.world > 1:
             views = [p.ref_image_id for p in self.problems]
@@ -402,7 +407,11 @@ class Pipeline:
             for v in views:
                 if owners[v] != self.rank:
                     self.store.shapes[(key, v)] = self._pass_shape(v)
-            self.exchange.share(key, views, owners, self.store)
+            t1 = time.perf_counter()
+            with self._timed("exchange"):
+                self.exchange.share(key, views, owners, self.store)
+            log.exchange_s = time.perf_counter() - t1
+            log.exchange_bytes = sum(4 * int(np.prod(self.store.shapes[(key, v)])) for v in views)
         self.passes.append(log)
         self.pass_index += 1
 

@@ -59,12 +59,15 @@ def eval_nb_flop_per_pixel(model: str, V: int, samples: int = 36) -> float:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--mode", choices=["patchmatch", "pipeline"], default="patchmatch",
+                    help="patchmatch: the headline RunPatchMatch metric; pipeline: the sharded multi-pass schedule")
+    ap.add_argument("--views", type=int, default=24, help="pipeline mode: views in the capture")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--width", type=int, default=2000)
-    ap.add_argument("--height", type=int, default=1500)
-    ap.add_argument("--n-src", type=int, default=4)
-    ap.add_argument("--model", choices=["sphere", "pinhole"], default="sphere")
+    ap.add_argument("--width", type=int, default=None, help="default 2000 (pipeline mode: 3200)")
+    ap.add_argument("--height", type=int, default=None, help="default 1500 (pipeline mode: 2133)")
+    ap.add_argument("--n-src", type=int, default=None, help="default 4 (pipeline mode: 20)")
+    ap.add_argument("--model", choices=["sphere", "pinhole"], default=None, help="default sphere (pipeline: pinhole)")
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--math", choices=["exact", "fast"], default="fast",
@@ -79,7 +82,12 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true", help="skip the end-to-end ProcessProblem schedule timing")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_propagate.json"),
                     help="rocprofv3 PMC summary giving HBM bytes per propagation launch")
-    return ap.parse_args()
+    a = ap.parse_args()
+    pipe = a.mode == "pipeline"        # BASELINE.json configs[3] shape vs the headline metric's
+    for k, head, pl in (("width", 2000, 3200), ("height", 1500, 2133), ("n_src", 4, 20), ("model", "sphere", "pinhole")):
+        if getattr(a, k) is None:
+            setattr(a, k, pl if pipe else head)
+    return a
 
 
 def make_scene(args, rank: int):
@@ -200,8 +208,103 @@ def cpu_baseline(args, sc, params, gpu_rate_check=None):
     }
 
 
+def depth_exchange(args, ctx, rank, world, device, dist, allmax, reps=5):
+    """Every rank broadcasts its last depth map (W x H float32, acmmp_export_depth: HBM to HBM) to all
+    ranks in one grouped RCCL call -- what pipeline.RcclExchange does between two passes.  The RCCL
+    unique id travels over the bench's gloo group.  Returns timing and bandwidth (max over ranks), or
+    the error text: this side measurement never fails the bench."""
+    try:
+        uid = [capi.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = capi.Comm(device, uid[0], world, rank)
+        bufs = [capi.DeviceBuffer(device, (args.height, args.width)) for _ in range(world)]
+        ctx.export_depth(bufs[rank])
+        comm.broadcast(bufs, list(range(world)))                     # warm-up
+        ok = all(np.isfinite(b.download()).mean() > 0.5 for b in bufs)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            comm.broadcast(bufs, list(range(world)))
+        dt = allmax((time.perf_counter() - t0) / reps)
+        comm.close()
+        for b in bufs:
+            b.free()
+        nbytes = 4 * args.width * args.height
+        return {"ms_per_exchange": round(dt * 1e3, 3), "maps": world, "MB_per_map": round(nbytes / 1e6, 2),
+                "received_GBps_per_rank": round(nbytes * (world - 1) / dt / 1e9, 2), "maps_finite": bool(ok),
+                "transport": "RCCL grouped ncclBroadcast over xGMI (acmmp_comm_broadcast)"}
+    except Exception as e:                                           # noqa: BLE001
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
+def pipeline_mode(args, rank, world, local_rank, barrier, allmax):
+    """`--mode pipeline`: main.cpp's multi-scale ProcessProblem schedule (planar -> geom -> geom-multi,
+    JBU, hierarchy planar -> geom -> geom-multi) over a synthetic multi-view capture in the ETH3D-style
+    shape of BASELINE.json configs[3] (pinhole, ~20 sources per view, planar prior + multi-scale),
+    reference views sharded over the ranks (one GPU each), the depth maps of every pass exchanged
+    HBM-to-HBM over RCCL (pipeline.RcclExchange) before the next.  One JSON line: views/s of the
+    whole job, per-pass compute and exchange wall time (max over ranks), host stage totals."""
+    from acmmp import io, pipeline
+    ndev = capi.device_count()
+    if world > 1 and ndev and world > ndev:
+        raise SystemExit(f"bench --mode pipeline: {world} ranks on {ndev} GPU(s); RCCL needs one GPU per rank")
+    device = local_rank % ndev if ndev else local_rank
+    make = scene.pinhole_scene if args.model == "pinhole" else scene.sphere_scene
+    t_scene = time.perf_counter()
+    sc = make(args.width, args.height, n_src=args.views - 1, seed=args.seed)
+    scene_s = time.perf_counter() - t_scene
+    centres = np.array([-(np.asarray(c["R"], np.float64).reshape(3, 3).T @ np.asarray(c["t"], np.float64))
+                        for c in sc.cameras])
+    problems = []
+    for i in range(args.views):
+        pr = io.Problem(i)
+        others = sorted((j for j in range(args.views) if j != i),
+                        key=lambda j: (float(np.linalg.norm(centres[j] - centres[i])), j))
+        pr.src_image_ids = others[:args.n_src]
+        problems.append(pr)
+    ds = pipeline.Dataset({i: np.asarray(sc.images[i], np.float32) for i in range(args.views)},
+                          {i: np.array(sc.cameras[i], copy=True) for i in range(args.views)}, problems)
+    exchange = pipeline.rcclexchange_from_env(device) if world > 1 else pipeline.LocalExchange()
+    pipe = pipeline.Pipeline(ds, exchange=exchange, device=device, seed=args.seed,
+                             order="snapshot" if world > 1 else "reference", math=args.math)
+    barrier()
+    t0 = time.perf_counter()
+    pipe.run()
+    pipe.engine.synchronize()
+    elapsed = time.perf_counter() - t0
+    t_max = allmax(elapsed)
+    passes = [{"name": p.name, "compute_ms": round(allmax(p.compute_s) * 1e3, 1),
+               "exchange_ms": round(allmax(p.exchange_s) * 1e3, 2),
+               "exchange_MB": round(p.exchange_bytes / 1e6, 1)} for p in pipe.passes]
+    acc = [scene.depth_accuracy(pipe.store.get("depths_geom", v), sc.gt_depth)
+           for v in [0] if pipe.owner(0) == rank]
+    stages = {k: round(allmax(v), 3) for k, v in sorted(pipe.stage_s.items())}
+    n_gpus = min(world, ndev) if ndev else world
+    line = {
+        "metric": "ProcessProblem schedule throughput (views/s), sharded views + RCCL depth exchange",
+        "value": round(args.views / t_max, 4), "unit": "views/s", "n_gpus": n_gpus, "ranks": world,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32", "math": args.math,
+        "data": f"synthetic ({args.model.upper()} ring rig, ray-cast textured scene; no dataset reachable)",
+        "config": {"workload": f"{args.views} views {args.width}x{args.height} {args.model}, {args.n_src} sources "
+                               f"each (nearest centres), planar prior + multi-scale (main.cpp schedule)",
+                   "views": args.views, "width": args.width, "height": args.height, "n_src": args.n_src,
+                   "model": args.model, "parallelism": f"views-sharded x{world}, RCCL depth exchange"},
+        "total_s": round(t_max, 3), "ms_per_view": round(t_max / args.views * 1e3, 1),
+        "passes": passes, "stages_s": stages,
+        "exchange": "pipeline.RcclExchange (grouped ncclBroadcast, HBM to HBM)" if world > 1 else
+                    "none: one rank holds every view (no scaling curve from this run)",
+        "scene_s": round(scene_s, 1),
+        "quality": {"view0_frac_within_1pct_gt": round(float(acc[0]), 4) if acc else None},
+    }
+    exchange.close()
+    pipe.engine.close()
+    return line
+
+
 def main():
     args = parse()
+    if args.mode == "pipeline":
+        return main_pipeline(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -351,6 +454,12 @@ def main():
         "note": "FP32 vector peak (equal to the f32 MFMA dense peak); the path has no GEMM-shaped work",
     }
 
+    # the pipeline's one exchange step: after a pass every rank's depth map reaches every
+    # other rank -- a grouped RCCL broadcast of each rank's map, HBM to HBM, outside the timed region
+    exch = None
+    if world > 1 and ndev and world <= ndev and os.environ.get("ACMMP_BENCH_EXCHANGE", "1") != "0":
+        exch = depth_exchange(args, ctx, rank, world, local_rank % ndev, dist, allmax)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, sc, params)
@@ -397,9 +506,38 @@ def main():
             "cpu_baseline": cpu,
             "nondegenerate_variant": variant,
             "end_to_end": e2e,
+            "depth_exchange": exch,
         }
         print(json.dumps(line), flush=True)
     ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def main_pipeline(args):
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        dist.init_process_group("gloo")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def allmax(x: float) -> float:
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    line = pipeline_mode(args, rank, world, local_rank, barrier, allmax)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
