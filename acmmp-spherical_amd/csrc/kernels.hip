@@ -243,6 +243,18 @@ __device__ __forceinline__ float depth_from_plane(float4 ph, float4 d) {
 // returns 0 there, this returns NaN and the sample's cost is 2.0).  Not bit-identical to the
 // oracle: parity is the tolerance of SURVEY.md §8c (tests/test_gpu_fastmath.py).
 
+#ifndef ACMMP_FM_GUARD
+#define ACMMP_FM_GUARD 0                    // fast mode: the |t| < 1e-6 test costs 3 VALU per view-sample
+#endif                                      // (r02 A/B profiles/r02_micro_ab.txt: metric +2%, C3 +1.8%)
+// Chunks whose VB views are all present compile without per-view guards (one basic block per sample):
+// pinhole +17% at C2 (V = 10: its 8-view chunk), SPHERE -1..-2% (longer live ranges), so pinhole only
+#ifndef ACMMP_FULL_CHUNK_PIN
+#define ACMMP_FULL_CHUNK_PIN 1
+#endif
+#ifndef ACMMP_FULL_CHUNK_SPH
+#define ACMMP_FULL_CHUNK_SPH 0
+#endif
+
 // atan(t) on [0, 1]: t + t^3 P(t^2), 7-term minimax, max |error| 1.1e-7 rad
 __device__ __forceinline__ float atan_core_fast(float t) {
     const float z = t * t;
@@ -278,7 +290,10 @@ __device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float&
         const float lon = copysignf(r, tx);
         ox = fmaf(lon, c.fkx, c.cx);
         oy = fmaf(neg_lat, c.fky, c.cy);
-        if (r2 < 1e-12f) { ox = c.cx; oy = c.cy; }            // |t| < 1e-6 (:618-622)
+        // |t| < 1e-6 (:618-622): a sample on a source camera's centre.  ACMMP_FM_GUARD 0 drops the
+        // test: such a sample then projects to NaN and its view's cost is 2.0 (the NCC clamp) -- the
+        // reference's tex2D of (cx, cy) there is as meaningless, and no real geometry reaches it
+        if (ACMMP_FM_GUARD && r2 < 1e-12f) { ox = c.cx; oy = c.cy; }
     } else {
         // K (R P + t) = (K R) P + K t, rows 0-1; the perspective divide by z = R[6..8] P + t[2]
         const float hx = fmaf(c.KR[2], P.z, fmaf(c.KR[1], P.y, fmaf(c.KR[0], P.x, c.Kt[0])));
@@ -576,9 +591,10 @@ constexpr int kPipeG16 = ACMMP_PIPEG16;
 #define ACMMP_RC_CONST_PIPE 0               // 1: PIPE callers (k_eval_ref) also read the reference camera per sample (A/B r01_v27: -3%)
 #endif
 
-template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM = 0>
+template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM = 0, bool FULL = false>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
-                                          const int (&vlist)[VB], int nv, float (&cost)[VB]) {
+                                          const int (&vlist)[VB], int nv_rt, float (&cost)[VB]) {
+    const int nv = FULL ? VB : nv_rt;           // FULL: every view of the chunk present (compile-time)
     // SPHERE: the weight sum of every view is the pixel's patch sum (hypothesis- and view-independent);
     // below 1e-6 each cost is 2.0 (ACMMP.cu:501-503) whatever the samples, so they are not evaluated.
     // (The SPHERE sigma-in-radians band of SURVEY.md §0.5 puts ~40% of a 2000x1500 view here.)
@@ -827,7 +843,10 @@ __device__ __forceinline__ void for_all_views_t(const KParams& kp, int px, int p
         }
         if (nv == 0) break;
         float cost[VB];
-        ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM>(kp, px, py, pt, ph, vlist, nv, cost);
+        if ((MODEL == kSphere ? ACMMP_FULL_CHUNK_SPH : ACMMP_FULL_CHUNK_PIN) && VB > 1 && nv == VB)
+            ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM, true>(kp, px, py, pt, ph, vlist, nv, cost);
+        else
+            ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM>(kp, px, py, pt, ph, vlist, nv, cost);
 #pragma unroll
         for (int k = 0; k < VB; ++k)
             if (k < nv) f(vlist[k] - 1, cost[k]);
