@@ -23,6 +23,7 @@ ARCH = os.environ.get("ACMMP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["kernels.hip", "capi.cpp", "comm.cpp", "fusion.cpp", "planar_prior.cpp"]
+KERNEL_TUS = 5            # kernels.hip is compiled once per ACMMP_TU value in parallel (see its header)
 HIP_CPP = {"capi.cpp", "comm.cpp", "fusion.cpp", "planar_prior.cpp"}              # host C++ that includes HIP headers
 HEADERS = ["engine.h", "detmath.h", "planar.h"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize", f"--offload-arch={ARCH}",
@@ -43,13 +44,16 @@ def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines=(),
     objdir = objdir or os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
     objs, cmds = [], []
-    for src in SOURCES:
-        obj = os.path.join(objdir, src + ".o")
+    units = [(src, None) for src in SOURCES if src != "kernels.hip"]
+    units = [("kernels.hip", tu) for tu in range(KERNEL_TUS)] + units
+    for src, tu in units:
+        obj = os.path.join(objdir, src + (f".tu{tu}" if tu is not None else "") + ".o")
         srcp = os.path.join(CSRC, src)
         hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "acmmp.h")]
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < _newest([srcp] + hdrs):
             lang = ["-x", "hip"] if src in HIP_CPP else []
-            cmds.append([HIPCC, *COMMON, *flags, *[f"-D{d}" for d in defines], *lang, "-c", srcp, "-o", obj])
+            tud = [f"-DACMMP_TU={tu}"] if tu is not None else []
+            cmds.append([HIPCC, *COMMON, *flags, *[f"-D{d}" for d in defines], *tud, *lang, "-c", srcp, "-o", obj])
         objs.append(obj)
 
     def compile_one(cmd):
@@ -57,7 +61,7 @@ def build(force: bool = False, verbose: bool = True, lib: str = LIB, defines=(),
             print("[acmmp build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
 
-    with ThreadPoolExecutor(max_workers=min(len(cmds), 4) or 1) as ex:
+    with ThreadPoolExecutor(max_workers=min(len(cmds), max(1, min(8, os.cpu_count() or 1)))) as ex:
         list(ex.map(compile_one, cmds))
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs, "-L/opt/rocm/lib", "-lrccl",
            "-Wl,-rpath,/opt/rocm/lib"]

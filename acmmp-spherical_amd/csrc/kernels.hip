@@ -22,6 +22,14 @@
 #include "engine.h"
 #include "planar.h"
 
+// Translation-unit split: build.py compiles this file once per ACMMP_TU value (0..kTUs-1), in
+// parallel, and every kernel instance and host launcher lands in exactly one of those objects.  With
+// ACMMP_TU unset the whole file is one unit.
+#ifndef ACMMP_TU
+#define ACMMP_TU -1
+#endif
+#define ACMMP_IN_TU(n) (ACMMP_TU < 0 || ACMMP_TU == (n))
+
 namespace acmmp {
 
 // ------------------------------------------------------------------ RNG
@@ -868,6 +876,22 @@ __device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py,
     }
 }
 
+// TF: the texel format and math mode as one compile-time choice, so each kernel instance gets its own
+// register allocation (k_eval_nb's r02 A/B: a run-time branch between them sized every path for the
+// largest).  0 = fp32 texels, math mode at run time (images that are not binary16-exact); 1 = binary16
+// texels, exact; 2 = binary16 texels, fast math.
+template <int MODEL, int VB, int STAGED, bool PIPE, int TF, bool PIPE_FM = PIPE, typename F>
+__device__ __forceinline__ void for_all_views_tf(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
+                                                 uint32_t wave_mask, F&& f) {
+    if constexpr (TF == 0) {
+        if (kp.fast) for_all_views_t<MODEL, VB, STAGED, PIPE_FM, 0, 1>(kp, px, py, pt, ph, wave_mask, f);
+        else for_all_views_t<MODEL, VB, STAGED, PIPE, 0, 0>(kp, px, py, pt, ph, wave_mask, f);
+    } else {
+        for_all_views_t<MODEL, VB, STAGED, TF == 2 ? PIPE_FM : PIPE, 1, TF == 2 ? 1 : 0>(kp, px, py, pt, ph, wave_mask, f);
+    }
+}
+static inline int tf_of(const KParams& kp) { return kp.tex16 ? (kp.fast ? 2 : 1) : 0; }
+
 __device__ __forceinline__ float vw_get(const uint32_t (&vwp)[4], int v) {
     const uint32_t word = v < 8 ? vwp[0] : (v < 16 ? vwp[1] : (v < 24 ? vwp[2] : vwp[3]));
     return static_cast<float>((word >> ((v & 7) * 4)) & 15u);
@@ -916,6 +940,7 @@ static inline unsigned eval_grid(long long nblocks) {
 
 // ------------------------------------------------------------------ kernels: setup
 
+#if ACMMP_IN_TU(0)
 __global__ void k_to_f16(const float* __restrict__ src, long long n, uint16_t* __restrict__ dst,
                          int* __restrict__ inexact) {
     const long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -1006,6 +1031,8 @@ __global__ void k_spatial(const KParams kp, float* __restrict__ spatial) {
     }
 }
 
+#endif  // ACMMP_IN_TU(0)
+
 // ------------------------------------------------------------------ initial cost
 
 __device__ __forceinline__ void sort_small(float* d, int n) {
@@ -1018,14 +1045,14 @@ __device__ __forceinline__ void sort_small(float* d, int n) {
 }
 
 // ComputeMultiViewInitialCostandSelectedViews, ACMMP.cu:519-556
-template <int MODEL, int VB, int VMAXB = VB>
+template <int MODEL, int VB, int VMAXB, int TF>
 __device__ float initial_cost(const KParams& kp, int px, int py, const Patch& pt, float4 ph, uint32_t* sel,
                               float* cvec = nullptr) {
     constexpr int VMAX = VMAXB < 8 ? VMAXB : kMaxViews;      // pick_vb: V <= VMAXB when VMAXB < 8
     float cv[VMAX], cvc[VMAX];
     int nvalid = 0;
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
-    for_all_views<MODEL, VB, 0, true>(kp, px, py, pt, ph, all, [&](int v, float c) {
+    for_all_views_tf<MODEL, VB, 0, true, TF>(kp, px, py, pt, ph, all, [&](int v, float c) {
         cv[v] = c;
         cvc[v] = c;
         if (c < 2.0f) nvalid++;
@@ -1070,9 +1097,9 @@ enum InitBranch { kInitRandom = 0, kInitPlanar = 1, kInitUpsample = 2, kInitReus
 #ifndef ACMMP_INIT_VB
 #define ACMMP_INIT_VB 2
 #endif
-constexpr int kInitVB = ACMMP_INIT_VB;
+[[maybe_unused]] constexpr int kInitVB = ACMMP_INIT_VB;
 
-template <int MODEL, int VB, int BR, int VMAXB>
+template <int MODEL, int VB, int BR, int VMAXB, int TF>
 __global__ __launch_bounds__(256) void k_init(const KParams kp) {
     // 16x16 tiles in XCD-aware order (xcd_block) over a row-major grid of ceil(W/16) tiles per row
     const long long tile = xcd_block(blockIdx.x);
@@ -1096,7 +1123,7 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
         const float depth = fmaf(rs.uniform(), kp.depth_max - kp.depth_min, kp.depth_min);
         ph = random_normal(dc, rs);
         ph.w = dist_to_origin(dc, depth, ph);
-        cost = initial_cost<MODEL, VB, VMAXB>(kp, x, y, pt, ph, &sel, cvec);
+        cost = initial_cost<MODEL, VB, VMAXB, TF>(kp, x, y, pt, ph, &sel, cvec);
     } else if (BR == kInitPlanar) {
         if (kp.mask[center] > 0 && kp.costs_rm[center] >= 0.1f) {
             const float perturbation = 0.02f;
@@ -1112,7 +1139,7 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
             const float depth = ph.w;
             ph.w = dist_to_origin(dc, depth, ph);
         }
-        cost = initial_cost<MODEL, VB, VMAXB>(kp, x, y, pt, ph, &sel, cvec);
+        cost = initial_cost<MODEL, VB, VMAXB, TF>(kp, x, y, pt, ph, &sel, cvec);
     } else if (BR == kInitUpsample) {
         const float scale = static_cast<float>(1.0 * static_cast<double>(kp.scaled_cols) / static_cast<double>(kp.W));
         const float sigmad = 0.50f, sigmar = 25.5f;
@@ -1146,16 +1173,16 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
         normalize3(nx, ny, nz);
         const float4 cur = kp.planes_rm[center];
         uint32_t sel0;
-        kp.pre_rm[center] = initial_cost<MODEL, VB, VMAXB>(kp, x, y, pt, cur, &sel0);
+        kp.pre_rm[center] = initial_cost<MODEL, VB, VMAXB, TF>(kp, x, y, pt, cur, &sel0);
         ph = to_ref(rc, make_float4(nx, ny, nz, 0.0f));
         ph.w = dist_to_origin(dc, cur.w, ph);
-        cost = initial_cost<MODEL, VB, VMAXB>(kp, x, y, pt, ph, &sel, cvec);
+        cost = initial_cost<MODEL, VB, VMAXB, TF>(kp, x, y, pt, ph, &sel, cvec);
     } else {
         ph = kp.hier ? kp.scaled[center] : kp.planes_rm[center];
         ph = to_ref(rc, ph);
         const float depth = ph.w;
         ph.w = dist_to_origin(dc, depth, ph);
-        cost = initial_cost<MODEL, VB, VMAXB>(kp, x, y, pt, ph, &sel, cvec);
+        cost = initial_cost<MODEL, VB, VMAXB, TF>(kp, x, y, pt, ph, &sel, cvec);
     }
     kp.plane_cs[colour][ci] = ph;
     kp.cost_cs[colour][ci] = cost;
@@ -1426,6 +1453,7 @@ constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 la
 #ifndef ACMMP_PICK_PASS
 #define ACMMP_PICK_PASS 1
 #endif
+#if ACMMP_IN_TU(0)
 __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour) {
     const long long q = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
     const int d = blockIdx.y;
@@ -1434,6 +1462,8 @@ __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour
     const long long ci = static_cast<long long>(py) * kp.Wh + (px >> 1);
     kp.nbpos[d * kp.Pc + ci] = pick_neighbour(kp, d, px, py);
 }
+
+#endif  // ACMMP_IN_TU(0)
 
 #ifndef ACMMP_NB_WAVES
 #define ACMMP_NB_WAVES 8                    // k_eval_nb (SPHERE): minimum waves per SIMD the register budget must allow
@@ -1812,7 +1842,7 @@ __global__ __launch_bounds__(256, ACMMP_SEL_WAVES) void k_select(const KParams k
 }
 
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
-template <int MODEL, int VB, bool GEOM>
+template <int MODEL, int VB, bool GEOM, int TF>
 __global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_SPH : ACMMP_REF_WAVES) void k_eval_ref(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
@@ -1861,7 +1891,7 @@ __global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_
     float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
     for (int v = 0; v < kp.V; ++v)
         if (!((amask >> v) & 1u)) vcost[v * Pc] = __builtin_nanf("");
-    for_all_views<MODEL, VBA, kStaged, ACMMP_REF_PIPE>(kp, px, py, pt, tp, amask, [&](int v, float c) {
+    for_all_views_tf<MODEL, VBA, kStaged, ACMMP_REF_PIPE, TF>(kp, px, py, pt, tp, amask, [&](int v, float c) {
         vcost[v * Pc] = c;
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
@@ -1894,7 +1924,7 @@ __global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_
 
 // The queued candidates' views [ref_split, V) (one lane per candidate, patch samples recomputed),
 // continuing the aggregate's fma chain in view order from k_eval_ref's partial sum.
-template <int MODEL, int VB, bool GEOM>
+template <int MODEL, int VB, bool GEOM, int TF>
 __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const int colour) {
     const unsigned n = *kp.surv_count;
     const long long Pc = kp.Pc;
@@ -1921,7 +1951,7 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
         float temp_cost = kp.cand_cost[h * Pc + ci];
         float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
         constexpr int VBT = (VB == 4 && ACMMP_REF_VBA == 2) ? 2 : (VB > kEvalVB ? kEvalVB : VB);
-        for_all_views<MODEL, VBT, 0, ACMMP_REF_PIPE>(kp, px, py, pt, tp, umask, [&](int v, float c) {
+        for_all_views_tf<MODEL, VBT, 0, ACMMP_REF_PIPE, TF>(kp, px, py, pt, tp, umask, [&](int v, float c) {
             vcost[v * Pc] = c;
             const float w = vw_get(vwp, v);
             if (w > 0.0f) {
@@ -2027,6 +2057,7 @@ __global__ void k_merge(const KParams kp, const int do_post) {
 }
 
 // CheckerboardFilter, ACMMP.cu:1366-1480 (in place; reads only the other colour)
+#if ACMMP_IN_TU(0)
 __global__ void k_filter(const KParams kp, const int colour) {
     const int kx = blockIdx.x * blockDim.x + threadIdx.x;
     const int py = blockIdx.y * blockDim.y + threadIdx.y;
@@ -2127,6 +2158,8 @@ __global__ void k_jbu(const float* __restrict__ ref, int W, int H, const float* 
     out[static_cast<long long>(y) * W + x] = total / nf;
 }
 
+#endif  // ACMMP_IN_TU(0)
+
 // Test hooks: NCC / geom cost of arbitrary (pixel, plane) queries against every source view.
 template <int MODEL, int VB>
 __global__ void k_debug(const KParams kp, int which, int n, const int* __restrict__ qx, const int* __restrict__ qy,
@@ -2153,6 +2186,7 @@ __global__ void k_debug(const KParams kp, int which, int n, const int* __restric
 
 static inline int cdiv(long long a, int b) { return static_cast<int>((a + b - 1) / b); }
 
+#if ACMMP_IN_TU(0)
 hipError_t launch_to_f16(const float* src, long long n, uint16_t* dst, int* inexact, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     k_to_f16<<<static_cast<unsigned>((n + 255) / 256), 256, 0, s>>>(src, n, dst, inexact);
@@ -2191,6 +2225,8 @@ hipError_t launch_spatial_table(const KParams& kp, float* spatial, hipStream_t s
     return hipGetLastError();
 }
 
+#endif  // ACMMP_IN_TU(0)
+
 // View-chunk width: the per-view accumulators live in registers (6 per view).
 static inline int pick_vb(int V) { return V <= 1 ? 1 : (V <= 2 ? 2 : (V <= 4 ? 4 : 8)); }
 
@@ -2212,53 +2248,102 @@ static inline int pick_vb(int V) { return V <= 1 ? 1 : (V <= 2 ? 2 : (V <= 4 ? 4
         }                                                                               \
     } while (0)
 
+#define ACMMP_DISPATCH_TF(KP, BODY)                                                     \
+    do {                                                                                \
+        const int tf_ = tf_of(KP);                                                      \
+        if (tf_ == 2) { constexpr int TF = 2; BODY; }                                   \
+        else if (tf_ == 1) { constexpr int TF = 1; BODY; }                              \
+        else { constexpr int TF = 0; BODY; }                                            \
+    } while (0)
+
+#if ACMMP_IN_TU(1)
 hipError_t launch_init(const KParams& kp, hipStream_t s) {
     dim3 blk(16, 16), grd(xcd_grid(static_cast<long long>(cdiv(kp.W, 16)) * cdiv(kp.H, 16)));
     // branch order of ACMMP.cu:686-793
     const int br = (!kp.geom && !kp.hier) ? kInitRandom : kp.planar ? kInitPlanar : kp.upsample ? kInitUpsample
                                                                                                  : kInitReuse;
-    if (br == kInitRandom) ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, kInitVB, kInitRandom, VBC><<<grd, blk, 0, s>>>(kp)));
+    if (br == kInitRandom) ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, kInitVB, kInitRandom, VBC, TF><<<grd, blk, 0, s>>>(kp))));
     else if (br == kInitPlanar)
-        ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, kInitVB, kInitPlanar, VBC><<<grd, blk, 0, s>>>(kp)));
+        ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, kInitVB, kInitPlanar, VBC, TF><<<grd, blk, 0, s>>>(kp))));
     else if (br == kInitUpsample)
-        ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, kInitVB, kInitUpsample, VBC><<<grd, blk, 0, s>>>(kp)));
-    else ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, kInitVB, kInitReuse, VBC><<<grd, blk, 0, s>>>(kp)));
+        ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, kInitVB, kInitUpsample, VBC, TF><<<grd, blk, 0, s>>>(kp))));
+    else ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_init<M, kInitVB, kInitReuse, VBC, TF><<<grd, blk, 0, s>>>(kp))));
     return hipGetLastError();
 }
 
-hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s, hipEvent_t* ev) {
+hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,
+                        float* out, hipStream_t s) {
+    dim3 blk(64), grd(cdiv(n, 64));
+    ACMMP_DISPATCH(kp.model, kp.V, (k_debug<M, VBC><<<grd, blk, 0, s>>>(kp, which, n, px, py, planes, out)));
+    return hipGetLastError();
+}
+
+#endif  // ACMMP_IN_TU(1)
+
+// The half-sweep's launches, each in its own translation unit (their kernels are the bulk of the
+// template instances); launch_propagate strings them together.
+hipError_t launch_eval_nb(const KParams& kp, int colour, hipStream_t s);
+hipError_t launch_select(const KParams& kp, int colour, int iter, hipStream_t s);
+hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s);
+
+#if ACMMP_IN_TU(2)
+hipError_t launch_eval_nb(const KParams& kp, int colour, hipStream_t s) {
     const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
     const size_t lds_nb = nb_lds_bytes(kp.model, kp.S, kp.nside);
+    const dim3 grd = eval_grid(cdiv(npix, kNbPix));
+    if (kp.fast) {
+        if (kp.tex16) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 1, 1><<<grd, 256, lds_nb, s>>>(kp, colour)));
+        else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 0, 1><<<grd, 256, lds_nb, s>>>(kp, colour)));
+    } else {
+        if (kp.tex16) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 1, 0><<<grd, 256, lds_nb, s>>>(kp, colour)));
+        else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 0, 0><<<grd, 256, lds_nb, s>>>(kp, colour)));
+    }
+    return hipGetLastError();
+}
+#endif  // ACMMP_IN_TU(2)
+
+#if ACMMP_IN_TU(3)
+hipError_t launch_select(const KParams& kp, int colour, int iter, hipStream_t s) {
+    const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
+    if (kp.geom) ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, true><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
+    else ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, false><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
+    return hipGetLastError();
+}
+#endif  // ACMMP_IN_TU(3)
+
+#if ACMMP_IN_TU(4)
+hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s) {
+    const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
     const size_t lds_ref = ACMMP_REF_LITE ? sizeof(float2) * kp.S * kRefPix : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
+    hipError_t e = hipSuccess;
+    if (kp.ref_split > 0 && (e = hipMemsetAsync(kp.surv_count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
+    const dim3 grd_ref = eval_grid(cdiv(npix, kRefPix));
+    if (kp.geom) ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, true, TF><<<grd_ref, 256, lds_ref, s>>>(kp, colour))));
+    else ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, false, TF><<<grd_ref, 256, lds_ref, s>>>(kp, colour))));
+    if (kp.ref_split > 0) {
+        // grid-stride over the queue (its length is known on the device only): at most 5 per pixel
+        const unsigned grd = static_cast<unsigned>(std::min<long long>(cdiv(5 * npix, 256), 8192));
+        if (kp.geom) ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, true, TF><<<grd, 256, 0, s>>>(kp, colour))));
+        else ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, false, TF><<<grd, 256, 0, s>>>(kp, colour))));
+    }
+    return hipGetLastError();
+}
+#endif  // ACMMP_IN_TU(4)
+
+#if ACMMP_IN_TU(0)
+hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s, hipEvent_t* ev) {
+    const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
     hipError_t e = hipSuccess;
 #define ACMMP_MARK(i) if (ev && (e = hipEventRecord(ev[i], s)) != hipSuccess) return e
     // k_pick sits outside the four timed buckets (rocprof lists it): the k_eval_nb bucket the bench's
     // roofline prices is that kernel alone
     if (ACMMP_PICK_PASS) k_pick<<<dim3(cdiv(npix, 256), 8), 256, 0, s>>>(kp, colour);
     ACMMP_MARK(0);
-    {
-        const dim3 grd = eval_grid(cdiv(npix, kNbPix));
-        if (kp.fast) {
-            if (kp.tex16) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 1, 1><<<grd, 256, lds_nb, s>>>(kp, colour)));
-            else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 0, 1><<<grd, 256, lds_nb, s>>>(kp, colour)));
-        } else {
-            if (kp.tex16) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 1, 0><<<grd, 256, lds_nb, s>>>(kp, colour)));
-            else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 0, 0><<<grd, 256, lds_nb, s>>>(kp, colour)));
-        }
-    }
+    if ((e = launch_eval_nb(kp, colour, s)) != hipSuccess) return e;
     ACMMP_MARK(1);
-    if (kp.geom) ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, true><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
-    else ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, false><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
+    if ((e = launch_select(kp, colour, iter, s)) != hipSuccess) return e;
     ACMMP_MARK(2);
-    if (kp.ref_split > 0 && (e = hipMemsetAsync(kp.surv_count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
-    if (kp.geom) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, true><<<eval_grid(cdiv(npix, kRefPix)), 256, lds_ref, s>>>(kp, colour)));
-    else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, false><<<eval_grid(cdiv(npix, kRefPix)), 256, lds_ref, s>>>(kp, colour)));
-    if (kp.ref_split > 0) {
-        // grid-stride over the queue (its length is known on the device only): at most 5 per pixel
-        const unsigned grd = static_cast<unsigned>(std::min<long long>(cdiv(5 * npix, 256), 8192));
-        if (kp.geom) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, true><<<grd, 256, 0, s>>>(kp, colour)));
-        else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, false><<<grd, 256, 0, s>>>(kp, colour)));
-    }
+    if ((e = launch_eval_ref(kp, colour, s)) != hipSuccess) return e;
     ACMMP_MARK(3);
     if (kp.model == kSphere) k_finish<kSphere><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, out);
     else k_finish<kPinhole><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, out);
@@ -2509,11 +2594,6 @@ hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int s
     return hipGetLastError();
 }
 
-hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,
-                        float* out, hipStream_t s) {
-    dim3 blk(64), grd(cdiv(n, 64));
-    ACMMP_DISPATCH(kp.model, kp.V, (k_debug<M, VBC><<<grd, blk, 0, s>>>(kp, which, n, px, py, planes, out)));
-    return hipGetLastError();
-}
+#endif  // ACMMP_IN_TU(0)
 
 }  // namespace acmmp
