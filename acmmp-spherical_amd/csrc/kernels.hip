@@ -139,6 +139,11 @@ __device__ __forceinline__ int cvt_i32(float x) {
     asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(x));
     return r;
 }
+__device__ __forceinline__ int cvt_flr_i32(float x) {             // cvt_i32(floorf(x)) in one instruction
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
 __device__ __forceinline__ int clamp_m1(int x, int hi) {          // clampi(x, -1, hi), hi wave-uniform
     int r;
     asm("v_med3_i32 %0, %1, -1, %2" : "=v"(r) : "v"(x), "s"(hi));
@@ -258,6 +263,9 @@ __device__ __forceinline__ float depth_from_plane(float4 ph, float4 d) {
 // pinhole +17% at C2 (V = 10: its 8-view chunk), SPHERE -1..-2% (longer live ranges), so pinhole only
 #ifndef ACMMP_FULL_CHUNK_PIN
 #define ACMMP_FULL_CHUNK_PIN 1
+#endif
+#ifndef ACMMP_VIEW_BARRIER
+#define ACMMP_VIEW_BARRIER 1
 #endif
 #ifndef ACMMP_FULL_CHUNK_SPH
 #define ACMMP_FULL_CHUNK_SPH 0
@@ -412,6 +420,9 @@ __device__ __forceinline__ float bilinear_pair(const float* img, int pitch, int 
 // several views in flight before consuming any.  SPHERE callers pass x already wrapped and y
 // clamped to [0, H-1] (never NaN), so y needs no clamp; x keeps clampi(f2i_sat(floor x), -1, W-1):
 // the float clamp below is the same map for every non-NaN value, and NaN -> 0 as f2i_sat does.
+#ifndef ACMMP_FRACT
+#define ACMMP_FRACT 1
+#endif
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 struct Tap {
     float a, b;
@@ -432,6 +443,23 @@ __device__ __forceinline__ Tap fetch_tap(__amdgpu_buffer_rsrc_t rs, Cam& c, floa
     Tap t;
     t.a = x - fx;
     t.b = y - fy;
+    if (TEX == 1 && ACMMP_TEX_PAIRS && ACMMP_FRACT) {
+        // the same footprint with v_fract_f32 / v_cvt_flr_i32_f32 (one instruction each instead of floor
+        // + sub / floor + cvt).  fract(x) = min(x - floor(x), 1 - 2^-24) equals x - floor(x) unless x is
+        // in (-2^-24, 0): a SPHERE x is wrapped (a negative one is sx - k W, a multiple of ulp(W) >= 2^-23)
+        // and y clamped to [0, H-1]; a pinhole sample outside [0, W) x [0, H) is never accumulated.
+        t.a = __builtin_amdgcn_fractf(x);
+        t.b = __builtin_amdgcn_fractf(y);
+        const unsigned ix4 = (static_cast<unsigned>(clamp_m1(cvt_flr_i32(x), c.Wm1)) << 2) + 4u;
+        if (Y_IN_RANGE) {
+            const unsigned off = mad_u24(static_cast<unsigned>(cvt_flr_i32(y)), c.pitch4, ix4);
+            t.pw = __builtin_amdgcn_raw_buffer_load_b64(rs, off, c.pitch4, 0);
+        } else {
+            const unsigned off = mad_u24(static_cast<unsigned>(clamp_m1(cvt_flr_i32(y), c.Hm1) + 1), c.pitch4, ix4);
+            t.pw = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+        }
+        return t;
+    }
     if (TEX == 1 && ACMMP_TEX_PAIRS) {
         // row-pair layout: word (X, Y) = (t(X, Y), t(X, Y + 1)); the footprint is the two words at
         // (ix + 1, iy + 1) and (ix + 2, iy + 1): one 8-byte load
@@ -602,7 +630,13 @@ constexpr int kPipeG16 = ACMMP_PIPEG16;
 template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM = 0, bool FULL = false>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv_rt, float (&cost)[VB]) {
-    const int nv = FULL ? VB : nv_rt;           // FULL: every view of the chunk present (compile-time)
+    // FULL: every view of the chunk present (compile-time); otherwise a wave-uniform count, kept in an
+    // SGPR so the per-view guards are scalar branches (without it they were lane masks round-tripped
+    // through a VGPR: two VALU per view-sample)
+#ifndef ACMMP_NV_UNIFORM
+#define ACMMP_NV_UNIFORM 1
+#endif
+    const int nv = FULL ? VB : (ACMMP_NV_UNIFORM ? uniform_int(nv_rt) : nv_rt);
     // SPHERE: the weight sum of every view is the pixel's patch sum (hypothesis- and view-independent);
     // below 1e-6 each cost is 2.0 (ACMMP.cu:501-503) whatever the samples, so they are not evaluated.
     // (The SPHERE sigma-in-radians band of SURVEY.md §0.5 puts ~40% of a 2000x1500 view here.)
@@ -681,7 +715,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
 #define ACMMP_ACCUMULATE(v)                                                  \
             do {                                                             \
                 const float sp = lerp_tap<TEX>(tap[v]);                      \
-                if (ok[v]) {                                                 \
+                if (MODEL == kSphere ? (v < nv) : ok[v]) {                   \
                     if (MODEL == kPinhole) {                                 \
                         sbw[v] += w;                                         \
                         sref[v] = fmaf(w, r, sref[v]);                       \
@@ -714,6 +748,9 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                     tap[v] = fetch_tap<TEX, MODEL == kSphere>(rs, c, sx, sy);
                     if (G == 1) ACMMP_ACCUMULATE(v);
                 }
+                // a full SPHERE chunk has no per-view branches; keep its views' code in view order
+                // (interleaved, their live ranges overlap and the 7-wave register budget spills)
+                if (FULL && MODEL == kSphere && ACMMP_VIEW_BARRIER) __builtin_amdgcn_sched_barrier(0);
                 // G > 1: views are consumed in groups of G, a group's texels all in flight before the
                 // first is used (PIPE: the whole chunk; ~6 VGPRs per view in flight)
                 if (G > 1 && ((v + 1) % G == 0 || v == VB - 1)) {

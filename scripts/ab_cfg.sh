@@ -1,0 +1,23 @@
+#!/bin/bash
+# A/B of library variants over several bench configs (GPU box, repo root): GPU tests on each TESTED lib,
+# then for each config two alternating rounds over ALL libs (fast math unless the config says otherwise).
+# Usage: bash scripts/ab_cfg.sh TAG "TESTED_LIBS" "ALL_LIBS" "CONFIG1" "CONFIG2" ...  (CONFIG "" = the metric)
+set -o pipefail
+export TMPDIR=/tmp
+TAG=$1; TESTED=$2; LIBS=$3; shift 3
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+BASE="--no-cpu-baseline --no-variant --no-pipeline --no-other-mode --steps 5 --warmup 2"
+for lib in $TESTED; do
+  ACMMP_LIB=$lib timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $OUT/pytest_$(basename $lib).log 2>&1 || { echo "pytest failed ($lib)"; tail -30 $OUT/pytest_$(basename $lib).log; exit 1; }
+  echo "$(basename $lib): $(tail -1 $OUT/pytest_$(basename $lib).log)"
+done
+for cfg in "$@"; do
+  for rep in 1 2; do
+    for lib in $LIBS; do
+      ACMMP_LIB=$lib timeout -k 10 300 python bench.py $BASE $cfg > $OUT/b.json 2> $OUT/b.err || { tail $OUT/b.err; exit 1; }
+      python -c "import json,os;d=json.load(open('$OUT/b.json'));print(os.path.basename('$lib'), '[$cfg]', d['value'], d['ms_per_step'], d['roofline']['half_sweep_kernels_ms'])" | tee -a $OUT/ab.txt
+    done
+  done
+done
+echo AB_DONE
