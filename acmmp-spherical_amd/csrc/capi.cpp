@@ -157,12 +157,30 @@ DevCam acmmp::make_devcam(const acmmp_camera& s) {
     // fast-math constants (float products of the camera's own values)
     d.fkx = static_cast<float>(s.width) * 0.159154936671257019f;
     d.fky = static_cast<float>(s.height) * 0.318309873342514038f;
-    for (int r = 0; r < 2; ++r) {
-        for (int k = 0; k < 3; ++k)
-            d.KR[3 * r + k] = std::fmaf(s.K[3 * r + 2], s.R[6 + k], std::fmaf(s.K[3 * r + 1], s.R[3 + k], s.K[3 * r] * s.R[k]));
-        d.Kt[r] = std::fmaf(s.K[3 * r + 2], s.t[2], std::fmaf(s.K[3 * r + 1], s.t[1], s.K[3 * r] * s.t[0]));
-    }
+    set_relative_frame(d, s, s);                      // own frame until the problem's reference is known
     return d;
+}
+
+void acmmp::set_relative_frame(DevCam& d, const acmmp_camera& ref, const acmmp_camera& s) {
+    double C0[3], M[9], b[3];
+    for (int k = 0; k < 3; ++k)                      // reference centre -R0^T t0
+        C0[k] = -(double(ref.R[k]) * ref.t[0] + double(ref.R[3 + k]) * ref.t[1] + double(ref.R[6 + k]) * ref.t[2]);
+    for (int r = 0; r < 3; ++r) {
+        for (int k = 0; k < 3; ++k)                  // R R0^T
+            M[3 * r + k] = double(s.R[3 * r]) * ref.R[3 * k] + double(s.R[3 * r + 1]) * ref.R[3 * k + 1] +
+                           double(s.R[3 * r + 2]) * ref.R[3 * k + 2];
+        b[r] = double(s.R[3 * r]) * C0[0] + double(s.R[3 * r + 1]) * C0[1] + double(s.R[3 * r + 2]) * C0[2] + s.t[r];
+    }
+    const bool pin = s.model != ACMMP_SPHERE;
+    for (int r = 0; r < 3; ++r) {
+        for (int k = 0; k < 3; ++k) {
+            const double v = pin ? double(s.K[3 * r]) * M[k] + double(s.K[3 * r + 1]) * M[3 + k] + double(s.K[3 * r + 2]) * M[6 + k]
+                                 : M[3 * r + k];
+            d.FR[3 * r + k] = static_cast<float>(v);
+        }
+        const double v = pin ? double(s.K[3 * r]) * b[0] + double(s.K[3 * r + 1]) * b[1] + double(s.K[3 * r + 2]) * b[2] : b[r];
+        d.Ft[r] = static_cast<float>(v);
+    }
 }
 
 extern "C" {
@@ -374,6 +392,7 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
         d.img16_bytes = static_cast<int>(2LL * tp * (s.width + 2) * (s.height + 2));
         d.pitch2 = 2 * (s.width + 2);
         d.dep_off = 0; d.dep_w = 1; d.dep_h = 1;
+        set_relative_frame(d, cams[0], s);
     }
     HIP_TRY(c, dalloc(c->d_cams, static_cast<size_t>(n)));
     HIP_TRY(c, hipMemcpy(c->d_cams, c->dcams.data(), sizeof(DevCam) * n, hipMemcpyHostToDevice));

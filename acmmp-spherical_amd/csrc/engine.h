@@ -52,7 +52,10 @@ struct DevCam {
     int pitch2;                     // bytes per padded binary16 row
     // fast-math projection constants (KParams::fast)
     float fkx, fky;                 // SPHERE: W / (2 pi), H / pi
-    float KR[6], Kt[2];             // PINHOLE: rows 0-1 of K * R and K * t
+    // the fast projection in the reference camera's frame: a source point is FR q + Ft for the
+    // camera-frame point q = depth * ray of the reference pixel, FR = K R R0^T and Ft = K (R C0 + t)
+    // (K = identity for SPHERE; R0, C0: the problem's reference camera, rounded once from doubles)
+    float FR[9], Ft[3];
 };
 
 // Per-pixel state handed from k_select to k_eval_ref / k_finish (80 bytes).
@@ -146,6 +149,7 @@ hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut ou
 hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s);
 // Reference Camera -> device camera (derived constants computed as DESIGN.md §2.3 says), capi.cpp.
 DevCam make_devcam(const acmmp_camera& cam);
+void set_relative_frame(DevCam& d, const acmmp_camera& ref, const acmmp_camera& cam);   // DevCam::FR / Ft
 
 // SimpleFusionKernel (ACMMP.cu:1662-1814) for reference view `ref` + compaction in pixel order:
 // out_dense/flags are P-sized scratch, block_counts ceil(P/256) ints.

@@ -284,12 +284,14 @@ __device__ __forceinline__ float atan_core_fast(float t) {
     return fmaf(t * z, p, t);
 }
 
+// P: the sample's point in the REFERENCE camera's frame (depth * ray); FR / Ft map it into the source
+// camera (DevCam::FR, set per problem), so no world point is formed per sample.
 template <int MODEL, typename Cam>
 __device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float& oy) {
     if (MODEL == kSphere) {
-        const float tx = fmaf(c.R[2], P.z, fmaf(c.R[1], P.y, fmaf(c.R[0], P.x, c.t[0])));
-        const float ty = fmaf(c.R[5], P.z, fmaf(c.R[4], P.y, fmaf(c.R[3], P.x, c.t[1])));
-        const float tz = fmaf(c.R[8], P.z, fmaf(c.R[7], P.y, fmaf(c.R[6], P.x, c.t[2])));
+        const float tx = fmaf(c.FR[2], P.z, fmaf(c.FR[1], P.y, fmaf(c.FR[0], P.x, c.Ft[0])));
+        const float ty = fmaf(c.FR[5], P.z, fmaf(c.FR[4], P.y, fmaf(c.FR[3], P.x, c.Ft[1])));
+        const float tz = fmaf(c.FR[8], P.z, fmaf(c.FR[7], P.y, fmaf(c.FR[6], P.x, c.Ft[2])));
         const float r2 = fmaf(tz, tz, fmaf(ty, ty, tx * tx));
         // -latitude = asin(ty / |t|) (ProjectonCamera_cu :626-630)
         const float s = __builtin_amdgcn_fmed3f(ty * __builtin_amdgcn_rsqf(r2), -1.0f, 1.0f);
@@ -311,14 +313,23 @@ __device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float&
         // reference's tex2D of (cx, cy) there is as meaningless, and no real geometry reaches it
         if (ACMMP_FM_GUARD && r2 < 1e-12f) { ox = c.cx; oy = c.cy; }
     } else {
-        // K (R P + t) = (K R) P + K t, rows 0-1; the perspective divide by z = R[6..8] P + t[2]
-        const float hx = fmaf(c.KR[2], P.z, fmaf(c.KR[1], P.y, fmaf(c.KR[0], P.x, c.Kt[0])));
-        const float hy = fmaf(c.KR[5], P.z, fmaf(c.KR[4], P.y, fmaf(c.KR[3], P.x, c.Kt[1])));
-        const float tz = fmaf(c.R[8], P.z, fmaf(c.R[7], P.y, fmaf(c.R[6], P.x, c.t[2])));
+        // K (R_rel P + b) rows 0-1; the perspective divide by its row 2
+        const float hx = fmaf(c.FR[2], P.z, fmaf(c.FR[1], P.y, fmaf(c.FR[0], P.x, c.Ft[0])));
+        const float hy = fmaf(c.FR[5], P.z, fmaf(c.FR[4], P.y, fmaf(c.FR[3], P.x, c.Ft[1])));
+        const float tz = fmaf(c.FR[8], P.z, fmaf(c.FR[7], P.y, fmaf(c.FR[6], P.x, c.Ft[2])));
         const float inv = __builtin_amdgcn_rcpf(tz);
         ox = hx * inv;
         oy = hy * inv;
     }
+}
+
+// The fast path's sample point in the reference camera's frame (project_fast maps it onward):
+// SPHERE depth * ray, PINHOLE depth-as-z (Get3DPointonWorld_cu's pinhole branch, :579-581)
+template <int MODEL, typename Cam>
+__device__ __forceinline__ float3 cam_point_fast(Cam& c, int x, int y, float depth, float4 d) {
+    if (MODEL == kSphere) return make_float3(d.x * depth, d.y * depth, d.z * depth);
+    return make_float3((depth * (static_cast<float>(x) - c.K[2])) * c.inv_fx,
+                       (depth * (static_cast<float>(y) - c.K[5])) * c.inv_fy, depth);
 }
 
 // ComputeDepthfromPlaneHypothesis with the hardware reciprocal
@@ -657,8 +668,8 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     ConstCam* ccams = (ConstCam*)(kp.cams);
 #define PCV(v) ccams[cv[v]]
     const float4 dc = ray_at<MODEL>(kp, px, py);
-    const float3 Pc3 = world_point_ray<MODEL>(rc, px, py, FM ? depth_from_plane_fast(ph, dc) : depth_from_plane(ph, dc),
-                                              dc);
+    const float3 Pc3 = FM ? cam_point_fast<MODEL>(rc, px, py, depth_from_plane_fast(ph, dc), dc)
+                          : world_point_ray<MODEL>(rc, px, py, depth_from_plane(ph, dc), dc);
 #pragma unroll
     for (int v = 0; v < VB; ++v) {
         sbw[v] = pt.sbw; sref[v] = pt.sref; srr[v] = pt.srr;
@@ -704,7 +715,9 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             // instead of 12 wave-uniform VGPRs held across the loop
             float3 P;
             const float dep = FM ? depth_from_plane_fast(ph, rw) : depth_from_plane(ph, rw);
-            if (!PIPE || ACMMP_RC_CONST_PIPE)
+            if (FM)
+                P = cam_point_fast<MODEL>(ccams[0], px + i, py + j, dep, rw);
+            else if (!PIPE || ACMMP_RC_CONST_PIPE)
                 P = world_point_ray<MODEL>(ccams[0], px + i, py + j, dep, rw);
             else
                 P = world_point_ray<MODEL>(rc, px + i, py + j, dep, rw);
