@@ -32,7 +32,9 @@ EXPORTS = [
     "acmmp_planar_prior_host", "acmmp_set_planar_prior_from_maps", "acmmp_download_planar_prior",
     "acmmp_upload_depths_device", "acmmp_upload_views_device", "acmmp_export_depth", "acmmp_device_alloc", "acmmp_device_free", "acmmp_memcpy",
     "acmmp_comm_unique_id", "acmmp_comm_create", "acmmp_comm_destroy", "acmmp_comm_broadcast",
-    "acmmp_comm_allreduce_max",
+    "acmmp_comm_allreduce_max", "acmmp_comm_band_exchange", "acmmp_run_patchmatch_band",
+    "acmmp_band_begin", "acmmp_band_sweep", "acmmp_band_sweeps_left", "acmmp_band_halo_ranges",
+    "acmmp_band_copy_rows", "acmmp_band_end",
     "acmmp_fusion_create", "acmmp_fusion_set_view", "acmmp_fusion_run", "acmmp_fusion_last_error",
     "acmmp_fusion_destroy",
 ]
@@ -100,6 +102,14 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_comm_destroy.argtypes = [vp]
     L.acmmp_comm_broadcast.argtypes = [vp, i32, vp, vp, vp]
     L.acmmp_comm_allreduce_max.argtypes = [vp, vp, i32]
+    L.acmmp_comm_band_exchange.argtypes = [vp, vp, i32, i32, i32]
+    L.acmmp_run_patchmatch_band.argtypes = [vp, vp, u64, i32, i32, i32, i32]
+    L.acmmp_band_begin.argtypes = [vp, u64, i32, i32]
+    L.acmmp_band_sweep.argtypes = [vp, C.POINTER(i32)]
+    L.acmmp_band_sweeps_left.argtypes = [vp]
+    L.acmmp_band_halo_ranges.argtypes = [vp, vp]
+    L.acmmp_band_copy_rows.argtypes = [vp, vp, i32, i32, i32]
+    L.acmmp_band_end.argtypes = [vp, i32]
     L.acmmp_fusion_create.argtypes = [i32, i32, vp, C.POINTER(vp)]
     L.acmmp_fusion_set_view.argtypes = [vp, i32, vp, vp, vp]
     L.acmmp_fusion_run.argtypes = [vp, i32, i32, vp, vp, i32, vp]
@@ -139,6 +149,7 @@ class Context:
         if rc != 0:
             raise AcmmpError(f"acmmp_create({device}) failed: {STATUS.get(rc, rc)}")
         self.h = h
+        self.device = device
         self.W = self.H = self.N = 0
         self._params = None
 
@@ -289,6 +300,22 @@ class Context:
                 raise ValueError("download_into: need C-contiguous float32 (H, W, 4) planes and (H, W) costs")
         self._check(self.L.acmmp_download(self.h, _p(planes), _p(costs)), "download")
 
+    def download_rows_into(self, planes, costs, row0: int, row1: int):
+        """D2H of rows [row0, row1) of the row-major outputs into caller-owned C-contiguous float32 arrays
+        (row1 - row0, W, 4) and (row1 - row0, W) -- a band's share of a split run (acmmp_band_*)."""
+        n = row1 - row0
+        for a, tail in ((planes, (4,)), (costs, ())):
+            if a.dtype != np.float32 or not a.flags.c_contiguous or a.shape != (n, self.W) + tail:
+                raise ValueError("download_rows_into: need C-contiguous float32 (rows, W, 4) and (rows, W)")
+        if not (0 <= row0 < row1 <= self.H):
+            raise ValueError("download_rows_into: rows outside the view")
+        pp, cp = self.device_outputs()
+        dev = self.device
+        _host_check(self.L.acmmp_memcpy(dev, _p(planes), C.c_void_p(pp + 16 * row0 * self.W), 16 * n * self.W, 1),
+                    "memcpy D2H")
+        _host_check(self.L.acmmp_memcpy(dev, _p(costs), C.c_void_p(cp + 4 * row0 * self.W), 4 * n * self.W, 1),
+                    "memcpy D2H")
+
     def download_aux(self):
         sel = np.empty((self.H, self.W), np.uint32)
         pre = np.empty((self.H, self.W), np.float32)
@@ -299,6 +326,39 @@ class Context:
         a, b = C.c_void_p(), C.c_void_p()
         self._check(self.L.acmmp_device_outputs(self.h, C.byref(a), C.byref(b)), "device_outputs")
         return a.value, b.value
+
+    # ---- row-band split of one view (acmmp_band_*, SURVEY.md §8e latency mode) ----
+    BAND_HALO = 23
+
+    def band_begin(self, seed: int, row0: int, row1: int):
+        self._check(self.L.acmmp_band_begin(self.h, seed, row0, row1), "band_begin")
+
+    def band_sweep(self) -> int:
+        colour = C.c_int32(0)
+        self._check(self.L.acmmp_band_sweep(self.h, C.byref(colour)), "band_sweep")
+        return colour.value
+
+    def band_sweeps_left(self) -> int:
+        return int(self.L.acmmp_band_sweeps_left(self.h))
+
+    def band_halo_ranges(self):
+        """((send_up), (recv_up), (send_down), (recv_down)) row ranges [a, b) after a half-sweep."""
+        r = np.zeros(8, np.int32)
+        self._check(self.L.acmmp_band_halo_ranges(self.h, _p(r)), "band_halo_ranges")
+        return tuple((int(r[2 * k]), int(r[2 * k + 1])) for k in range(4))
+
+    def band_copy_rows_from(self, src: "Context", colour: int, row_a: int, row_b: int):
+        self._check(self.L.acmmp_band_copy_rows(self.h, src.h, colour, row_a, row_b), "band_copy_rows")
+
+    def band_end(self, do_post: bool = True):
+        self._check(self.L.acmmp_band_end(self.h, int(do_post)), "band_end")
+
+    def run_patchmatch_band(self, seed: int, row0: int, row1: int, comm=None, rank_up: int = -1,
+                            rank_down: int = -1):
+        """One band of a view split over ranks, halo exchange over RCCL (comm: a Comm, or None for a
+        band covering the whole view)."""
+        self._check(self.L.acmmp_run_patchmatch_band(self.h, comm.h if comm is not None else None, seed, row0, row1,
+                                                     rank_up, rank_down), "run_patchmatch_band")
 
     def synchronize(self):
         self._check(self.L.acmmp_synchronize(self.h), "synchronize")
@@ -481,6 +541,9 @@ class Comm:
         nb = np.array([b.nbytes for b in bufs], np.uint64)
         rt = np.array(roots, np.int32)
         _host_check(self.L.acmmp_comm_broadcast(self.h, n, C.cast(ptrs, C.c_void_p), _p(nb), _p(rt)), "broadcast")
+
+    def band_exchange(self, ctx: "Context", colour: int, rank_up: int, rank_down: int):
+        _host_check(self.L.acmmp_comm_band_exchange(self.h, ctx.h, colour, rank_up, rank_down), "band_exchange")
 
     def allreduce_max(self, vals):
         v = np.ascontiguousarray(vals, np.float64).copy()

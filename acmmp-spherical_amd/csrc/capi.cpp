@@ -84,6 +84,11 @@ struct acmmp_ctx {
     unsigned long long work_busy = 0, work_total = 0;
     int klaunch[4] = {0, 0, 0, 0};
     int math = ACMMP_MATH_EXACT;                // acmmp_set_math
+    // row-band split (acmmp_band_*): the run in progress
+    bool band_active = false;
+    KParams band_kp{};
+    int band_lo = 0, band_hi = 0, band_sw = 0, band_nsw = 0;
+    int band_cur[2] = {0, 0};
     std::string err;
 };
 
@@ -573,7 +578,7 @@ acmmp_status acmmp_download_planar_prior(acmmp_ctx* c, float* prior, uint32_t* m
 // pixels of one colour inside the checkerboard grid (the half-sweep's work items)
 static unsigned long long colour_pixels(const acmmp_ctx* c, const KParams& kp, int colour) {
     unsigned long long n = 0;
-    for (int y = 0; y < kp.rows; ++y) {
+    for (int y = kp.row_lo; y < kp.row_hi; ++y) {
         const int first = (y + colour) & 1;                  // black = (x + y) even
         n += first < c->W ? static_cast<unsigned long long>((c->W - first + 1) / 2) : 0ull;
     }
@@ -617,6 +622,10 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.W = c->W; kp.H = c->H; kp.Wh = Wh_of(c); kp.N = c->N; kp.V = c->N - 1;
     kp.R = R; kp.inc = p.radius_increment; kp.nside = nside; kp.S = nside * nside;
     kp.rows = std::min(c->H, 32 * (((c->H / 2) + 15) / 16));
+    kp.row_lo = 0; kp.row_hi = kp.rows;
+    kp.init_lo = 0; kp.init_hi = c->H;
+    kp.merge_lo = 0; kp.merge_hi = c->H;
+    for (int k = 0; k < 2; ++k) { kp.filt_lo[k] = 0; kp.filt_hi[k] = kp.rows; }
     kp.dpitch = c->W + 2 * R;
     kp.depth_min = p.depth_min; kp.depth_max = p.depth_max;
     kp.sigma_spatial = p.sigma_spatial; kp.sigma_color = p.sigma_color;
@@ -761,6 +770,150 @@ acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx* c, uint64_t seed, int n_half_swe
 }
 
 acmmp_status acmmp_run_patchmatch(acmmp_ctx* c, uint64_t seed) { return acmmp_run_patchmatch_ex(c, seed, -1, 1); }
+
+// ------------------------------------------------------------------ row-band split
+//
+// One reference view over several contexts (GPUs), each updating the image rows [lo, hi) of the
+// checkerboard grid.  A pixel's update reads other pixels' plane / cost / selected views at most
+// ACMMP_BAND_HALO rows away (the far neighbour scan reaches 3 + 2 * 10 rows, ACMMP.cu:971-979), so after
+// each half-sweep a context receives the updated colour's rows [lo - 23, lo) and [hi, hi + 23) from its
+// neighbours; everything else a band reads is per pixel (init, RNG, images, priors) and is computed
+// locally on band +- halo.  The post stage needs the other colour within 5 rows for the median filter,
+// whose black pass feeds the red one: merge covers band +- 10 rows and the black filter band +- 5.  The
+// band's rows then equal the whole-view run's bit for bit (tests/test_gpu_band.py).
+
+}  // extern "C"
+
+namespace {
+
+void band_ranges(const KParams& kp, int lo, int hi, int& sup_a, int& sup_b, int& rup_a, int& rup_b, int& sdn_a,
+                 int& sdn_b, int& rdn_a, int& rdn_b) {
+    const int h = ACMMP_BAND_HALO, rows = kp.rows;
+    sup_a = std::min(lo, rows); sup_b = std::min(std::min(lo + h, hi), rows);        // to the band above
+    rup_a = std::min(std::max(0, lo - h), rows); rup_b = std::min(lo, rows);         // from it
+    sdn_a = std::min(std::max(lo, hi - h), rows); sdn_b = std::min(hi, rows);        // to the band below
+    rdn_a = std::min(hi, rows); rdn_b = std::min(hi + h, rows);                      // from it
+    if (lo == 0) sup_a = sup_b = rup_a = rup_b = 0;
+    if (hi >= kp.H) sdn_a = sdn_b = rdn_a = rdn_b = 0;
+}
+
+}  // namespace
+
+acmmp_status acmmp::band_buffers(acmmp_ctx* c, int colour, BandBuffers* b) {
+    if (!c || !b || colour < 0 || colour > 1) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (!c->band_active) return fail(c, ACMMP_ERR_STATE, "no band run in progress");
+    b->plane = c->d_plane_cs[colour][c->band_cur[colour]];
+    b->cost = c->d_cost_cs[colour][c->band_cur[colour]];
+    b->sel = c->d_sel_cs[colour];
+    b->Wh = c->band_kp.Wh;
+    b->stream = c->stream;
+    b->device = c->device;
+    return ACMMP_OK;
+}
+
+extern "C" {
+
+acmmp_status acmmp_band_begin(acmmp_ctx* c, uint64_t seed, int row0, int row1) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
+    if (row0 < 0 || row1 > c->H || row0 >= row1) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "band rows outside the image");
+    if (!(row0 == 0 && row1 == c->H) && row1 - row0 < ACMMP_BAND_HALO)
+        return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "a band must span at least ACMMP_BAND_HALO rows");
+    HIP_TRY(c, hipSetDevice(c->device));
+    KParams& kp = c->band_kp;
+    acmmp_status st = build_kparams(c, kp, seed);
+    if (st != ACMMP_OK) return st;
+    const int h = ACMMP_BAND_HALO, rows = kp.rows, H = c->H;
+    kp.row_lo = std::min(row0, rows); kp.row_hi = std::min(row1, rows);
+    kp.init_lo = std::max(0, row0 - h); kp.init_hi = std::min(H, row1 + h);
+    kp.merge_lo = std::max(0, row0 - 10); kp.merge_hi = std::min(H, row1 + 10);
+    kp.filt_lo[0] = std::min(std::max(0, row0 - 5), rows); kp.filt_hi[0] = std::min(row1 + 5, rows);
+    kp.filt_lo[1] = kp.row_lo; kp.filt_hi[1] = kp.row_hi;
+    const size_t Pc = static_cast<size_t>(kp.Pc);
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long) * 256, s));
+    HIP_TRY(c, hipEventRecord(c->ev[0], s));
+    HIP_TRY(c, launch_init(kp, s));
+    for (int k = 0; k < 2; ++k) {
+        HIP_TRY(c, hipMemcpyAsync(c->d_plane_cs[k][1], c->d_plane_cs[k][0], sizeof(float4) * Pc, hipMemcpyDeviceToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(c->d_cost_cs[k][1], c->d_cost_cs[k][0], sizeof(float) * Pc, hipMemcpyDeviceToDevice, s));
+    }
+    HIP_TRY(c, hipEventRecord(c->ev[1], s));
+    c->band_lo = row0; c->band_hi = row1;
+    c->band_sw = 0; c->band_nsw = 2 * c->params.max_iterations;
+    c->band_cur[0] = c->band_cur[1] = 0;
+    c->band_active = true;
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_band_sweep(acmmp_ctx* c, int* colour_out) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (!c->band_active) return fail(c, ACMMP_ERR_STATE, "band_begin first");
+    if (c->band_sw >= c->band_nsw) return fail(c, ACMMP_ERR_STATE, "every half-sweep of the run is done");
+    HIP_TRY(c, hipSetDevice(c->device));
+    KParams& kp = c->band_kp;
+    const int sw = c->band_sw, colour = sw & 1, iter = sw / 2;
+    int* cur = c->band_cur;
+    SweepOut out{c->d_plane_cs[colour][cur[colour] ^ 1], c->d_cost_cs[colour][cur[colour] ^ 1]};
+    HIP_TRY(c, launch_propagate(kp, colour, iter, out, c->stream, nullptr));
+    cur[colour] ^= 1;
+    kp.plane_cs[colour] = c->d_plane_cs[colour][cur[colour]];
+    kp.cost_cs[colour] = c->d_cost_cs[colour][cur[colour]];
+    ++c->band_sw;
+    if (colour_out) *colour_out = colour;
+    return ACMMP_OK;
+}
+
+int acmmp_band_sweeps_left(const acmmp_ctx* c) { return c && c->band_active ? c->band_nsw - c->band_sw : 0; }
+
+acmmp_status acmmp_band_halo_ranges(const acmmp_ctx* c, int ranges[8]) {
+    if (!c || !ranges) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (!c->band_active) return ACMMP_ERR_STATE;
+    band_ranges(c->band_kp, c->band_lo, c->band_hi, ranges[0], ranges[1], ranges[2], ranges[3], ranges[4], ranges[5],
+                ranges[6], ranges[7]);
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_band_copy_rows(acmmp_ctx* dst, acmmp_ctx* src, int colour, int row_a, int row_b) {
+    if (!dst || !src || dst == src) return ACMMP_ERR_INVALID_ARGUMENT;
+    BandBuffers d{}, s{};
+    acmmp_status st = band_buffers(dst, colour, &d);
+    if (st == ACMMP_OK) st = band_buffers(src, colour, &s);
+    if (st != ACMMP_OK) return st;
+    if (d.Wh != s.Wh || dst->H != src->H || row_a < 0 || row_b > dst->H || row_a > row_b)
+        return fail(dst, ACMMP_ERR_INVALID_ARGUMENT, "band contexts differ in size or rows out of range");
+    if (row_a == row_b) return ACMMP_OK;
+    // the source's half-sweep must be complete before its rows are read
+    HIP_TRY(src, hipSetDevice(src->device));
+    HIP_TRY(src, hipStreamSynchronize(src->stream));
+    HIP_TRY(dst, hipSetDevice(dst->device));
+    const size_t off = static_cast<size_t>(row_a) * d.Wh, n = static_cast<size_t>(row_b - row_a) * d.Wh;
+    HIP_TRY(dst, hipMemcpyAsync(d.plane + off, s.plane + off, sizeof(float4) * n, hipMemcpyDeviceToDevice, dst->stream));
+    HIP_TRY(dst, hipMemcpyAsync(d.cost + off, s.cost + off, sizeof(float) * n, hipMemcpyDeviceToDevice, dst->stream));
+    HIP_TRY(dst, hipMemcpyAsync(d.sel + off, s.sel + off, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, dst->stream));
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_band_end(acmmp_ctx* c, int do_post) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (!c->band_active) return fail(c, ACMMP_ERR_STATE, "band_begin first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    KParams& kp = c->band_kp;
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipEventRecord(c->ev[2], s));
+    HIP_TRY(c, launch_post(kp, do_post, s));
+    HIP_TRY(c, hipEventRecord(c->ev[3], s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    for (int k = 0; k < 2; ++k) {
+        if (c->band_cur[k]) {
+            std::swap(c->d_plane_cs[k][0], c->d_plane_cs[k][1]);
+            std::swap(c->d_cost_cs[k][0], c->d_cost_cs[k][1]);
+        }
+    }
+    for (int i = 0; i < 3; ++i) HIP_TRY(c, hipEventElapsedTime(&c->timing[i], c->ev[i], c->ev[i + 1]));
+    c->band_active = false;
+    return ACMMP_OK;
+}
 
 acmmp_status acmmp_download(acmmp_ctx* c, float* planes, float* costs) {
     if (!c) return ACMMP_ERR_INVALID_ARGUMENT;

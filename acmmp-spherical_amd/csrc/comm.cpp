@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "acmmp.h"
+#include "engine.h"
 
 static_assert(sizeof(ncclUniqueId) == ACMMP_COMM_ID_BYTES, "ncclUniqueId size");
 
@@ -127,6 +128,49 @@ acmmp_status acmmp_comm_allreduce_max(acmmp_comm* c, double* vals, int n) {
     TRY_HIP(hipMemcpyAsync(vals, c->d_scratch, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
     TRY_HIP(hipStreamSynchronize(c->stream));
     return ACMMP_OK;
+}
+
+acmmp_status acmmp_comm_band_exchange(acmmp_comm* c, acmmp_ctx* ctx, int colour, int rank_up, int rank_down) {
+    if (!c || !ctx || colour < 0 || colour > 1 || rank_up >= c->nranks || rank_down >= c->nranks ||
+        rank_up == c->rank || rank_down == c->rank)
+        return ACMMP_ERR_INVALID_ARGUMENT;
+    acmmp::BandBuffers b{};
+    acmmp_status st = acmmp::band_buffers(ctx, colour, &b);
+    if (st != ACMMP_OK) return st;
+    int r[8];
+    if ((st = acmmp_band_halo_ranges(ctx, r)) != ACMMP_OK) return st;
+    // (rows, peer, send?) for the four transfers; a band with no neighbour on one side has empty ranges
+    const int ops[4][4] = {{r[0], r[1], rank_up, 1}, {r[2], r[3], rank_up, 0}, {r[4], r[5], rank_down, 1},
+                           {r[6], r[7], rank_down, 0}};
+    TRY_HIP(hipSetDevice(b.device));
+    TRY_NCCL(ncclGroupStart());
+    for (const auto& op : ops) {
+        if (op[1] <= op[0]) continue;
+        if (op[2] < 0) { (void)ncclGroupEnd(); return ACMMP_ERR_INVALID_ARGUMENT; }
+        const size_t off = static_cast<size_t>(op[0]) * b.Wh, n = static_cast<size_t>(op[1] - op[0]) * b.Wh;
+        void* bufs[3] = {b.plane + off, b.cost + off, b.sel + off};
+        const size_t bytes[3] = {sizeof(float4) * n, sizeof(float) * n, sizeof(uint32_t) * n};
+        for (int k = 0; k < 3; ++k) {
+            const ncclResult_t res = op[3] ? ncclSend(bufs[k], bytes[k], ncclUint8, op[2], c->nccl, b.stream)
+                                           : ncclRecv(bufs[k], bytes[k], ncclUint8, op[2], c->nccl, b.stream);
+            if (res != ncclSuccess) { (void)ncclGroupEnd(); return ACMMP_ERR_COMM; }
+        }
+    }
+    TRY_NCCL(ncclGroupEnd());
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_run_patchmatch_band(acmmp_ctx* ctx, acmmp_comm* c, uint64_t seed, int row0, int row1,
+                                       int rank_up, int rank_down) {
+    if (!ctx || (!c && (rank_up >= 0 || rank_down >= 0))) return ACMMP_ERR_INVALID_ARGUMENT;
+    acmmp_status st = acmmp_band_begin(ctx, seed, row0, row1);
+    while (st == ACMMP_OK && acmmp_band_sweeps_left(ctx) > 0) {
+        int colour = 0;
+        st = acmmp_band_sweep(ctx, &colour);
+        if (st == ACMMP_OK && c) st = acmmp_comm_band_exchange(c, ctx, colour, rank_up, rank_down);
+    }
+    if (st != ACMMP_OK) return st;
+    return acmmp_band_end(ctx, 1);
 }
 
 }  // extern "C"

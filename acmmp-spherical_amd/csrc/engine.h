@@ -77,6 +77,11 @@ struct KParams {
     int W, H, Wh, N, V;             // ref size, colour row width ceil(W/2), images, source views
     int R, inc, nside, S;           // patch radius, radius_increment, offsets per axis, samples
     int rows;                       // rows the reference's checkerboard grid covers
+    // row ranges (full image by default; a row band in the split latency mode, acmmp_band_*):
+    int row_lo, row_hi;             // colour-grid rows the half-sweep kernels update, within [0, rows)
+    int init_lo, init_hi;           // rows k_init initialises, within [0, H)
+    int merge_lo, merge_hi;         // rows k_merge writes row-major, within [0, H)
+    int filt_lo[2], filt_hi[2];     // rows k_filter updates per colour, within [0, rows)
     int dpitch;                     // dir table pitch (W + 2R)
     float depth_min, depth_max, sigma_spatial, sigma_color;
     int top_k;
@@ -150,6 +155,16 @@ hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s);
 // Reference Camera -> device camera (derived constants computed as DESIGN.md §2.3 says), capi.cpp.
 DevCam make_devcam(const acmmp_camera& cam);
 void set_relative_frame(DevCam& d, const acmmp_camera& ref, const acmmp_camera& cam);   // DevCam::FR / Ft
+// Current working-state buffers of one colour of a band run (capi.cpp; comm.cpp exchanges their rows).
+struct BandBuffers {
+    float4* plane;
+    float* cost;
+    uint32_t* sel;
+    int Wh;
+    hipStream_t stream;
+    int device;
+};
+acmmp_status band_buffers(acmmp_ctx* c, int colour, BandBuffers* out);
 
 // SimpleFusionKernel (ACMMP.cu:1662-1814) for reference view `ref` + compaction in pixel order:
 // out_dense/flags are P-sized scratch, block_counts ceil(P/256) ints.

@@ -1155,8 +1155,8 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
     const long long tile = xcd_block(blockIdx.x);
     const int tiles_x = (kp.W + 15) >> 4;
     const int x = static_cast<int>(tile % tiles_x) * 16 + threadIdx.x;
-    const int y = static_cast<int>(tile / tiles_x) * 16 + threadIdx.y;
-    if (x >= kp.W || y >= kp.H) return;
+    const int y = kp.init_lo + static_cast<int>(tile / tiles_x) * 16 + threadIdx.y;
+    if (x >= kp.W || y >= kp.init_hi) return;
     const DevCam& rc = kp.cams[0];
     const long long center = static_cast<long long>(y) * kp.W + x;
     const int colour = (x + y) & 1;
@@ -1363,10 +1363,11 @@ __device__ __forceinline__ int pick_neighbour(const KParams& kp, int d, int px, 
 
 // Pixel q of the colour grid (row-major over rows x Wh); false when it does not exist.
 __device__ __forceinline__ bool colour_pixel(const KParams& kp, int colour, long long q, int& px, int& py) {
-    py = static_cast<int>(q / kp.Wh);
-    const int k = static_cast<int>(q - static_cast<long long>(py) * kp.Wh);
+    const int r = static_cast<int>(q / kp.Wh);
+    const int k = static_cast<int>(q - static_cast<long long>(r) * kp.Wh);
+    py = kp.row_lo + r;
     px = 2 * k + ((py + colour) & 1);
-    return py < kp.rows && px < kp.W;
+    return py < kp.row_hi && px < kp.W;
 }
 
 // Cooperative staging of the block's pixels: lane `h` of the `nh` lanes of pixel slot `lp`
@@ -2091,8 +2092,8 @@ __global__ __launch_bounds__(256) void k_finish(const KParams kp, const int colo
 template <int MODEL>
 __global__ void k_merge(const KParams kp, const int do_post) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y * blockDim.y + threadIdx.y;
-    if (x >= kp.W || y >= kp.H) return;
+    const int y = kp.merge_lo + static_cast<int>(blockIdx.y * blockDim.y + threadIdx.y);
+    if (x >= kp.W || y >= kp.merge_hi) return;
     const int colour = (x + y) & 1;
     const long long ci = cs_index(kp, x, y);
     const long long center = static_cast<long long>(y) * kp.W + x;
@@ -2110,9 +2111,9 @@ __global__ void k_merge(const KParams kp, const int do_post) {
 #if ACMMP_IN_TU(0)
 __global__ void k_filter(const KParams kp, const int colour) {
     const int kx = blockIdx.x * blockDim.x + threadIdx.x;
-    const int py = blockIdx.y * blockDim.y + threadIdx.y;
+    const int py = kp.filt_lo[colour] + static_cast<int>(blockIdx.y * blockDim.y + threadIdx.y);
     const int px = 2 * kx + ((py + colour) & 1);
-    if (py >= kp.rows || px >= kp.W) return;
+    if (py >= kp.filt_hi[colour] || px >= kp.W) return;
     const int width = kp.W, height = kp.H;
     const long long center = static_cast<long long>(py) * width + px;
     if (kp.costs_rm[center] < 0.001f) return;
@@ -2308,7 +2309,8 @@ static inline int pick_vb(int V) { return V <= 1 ? 1 : (V <= 2 ? 2 : (V <= 4 ? 4
 
 #if ACMMP_IN_TU(1)
 hipError_t launch_init(const KParams& kp, hipStream_t s) {
-    dim3 blk(16, 16), grd(xcd_grid(static_cast<long long>(cdiv(kp.W, 16)) * cdiv(kp.H, 16)));
+    if (kp.init_hi <= kp.init_lo) return hipSuccess;
+    dim3 blk(16, 16), grd(xcd_grid(static_cast<long long>(cdiv(kp.W, 16)) * cdiv(kp.init_hi - kp.init_lo, 16)));
     // branch order of ACMMP.cu:686-793
     const int br = (!kp.geom && !kp.hier) ? kInitRandom : kp.planar ? kInitPlanar : kp.upsample ? kInitUpsample
                                                                                                  : kInitReuse;
@@ -2338,7 +2340,7 @@ hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s);
 
 #if ACMMP_IN_TU(2)
 hipError_t launch_eval_nb(const KParams& kp, int colour, hipStream_t s) {
-    const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
+    const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
     const size_t lds_nb = nb_lds_bytes(kp.model, kp.S, kp.nside);
     const dim3 grd = eval_grid(cdiv(npix, kNbPix));
     if (kp.fast) {
@@ -2354,7 +2356,7 @@ hipError_t launch_eval_nb(const KParams& kp, int colour, hipStream_t s) {
 
 #if ACMMP_IN_TU(3)
 hipError_t launch_select(const KParams& kp, int colour, int iter, hipStream_t s) {
-    const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
+    const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
     if (kp.geom) ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, true><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
     else ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, false><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
     return hipGetLastError();
@@ -2363,7 +2365,7 @@ hipError_t launch_select(const KParams& kp, int colour, int iter, hipStream_t s)
 
 #if ACMMP_IN_TU(4)
 hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s) {
-    const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
+    const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
     const size_t lds_ref = ACMMP_REF_LITE ? sizeof(float2) * kp.S * kRefPix : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
     hipError_t e = hipSuccess;
     if (kp.ref_split > 0 && (e = hipMemsetAsync(kp.surv_count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
@@ -2382,7 +2384,7 @@ hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s) {
 
 #if ACMMP_IN_TU(0)
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s, hipEvent_t* ev) {
-    const long long npix = static_cast<long long>(kp.rows) * kp.Wh;
+    const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
     hipError_t e = hipSuccess;
 #define ACMMP_MARK(i) if (ev && (e = hipEventRecord(ev[i], s)) != hipSuccess) return e
     // k_pick sits outside the four timed buckets (rocprof lists it): the k_eval_nb bucket the bench's
@@ -2403,15 +2405,17 @@ hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut ou
 }
 
 hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s) {
-    {
-        dim3 blk(64, 4), grd(cdiv(kp.W, 64), cdiv(kp.H, 4));
+    if (kp.merge_hi > kp.merge_lo) {
+        dim3 blk(64, 4), grd(cdiv(kp.W, 64), cdiv(kp.merge_hi - kp.merge_lo, 4));
         if (kp.model == kSphere) k_merge<kSphere><<<grd, blk, 0, s>>>(kp, do_post);
         else k_merge<kPinhole><<<grd, blk, 0, s>>>(kp, do_post);
     }
     if (do_post) {
-        dim3 blk(64, 4), grd(cdiv(kp.Wh, 64), cdiv(kp.rows, 4));
-        k_filter<<<grd, blk, 0, s>>>(kp, 0);
-        k_filter<<<grd, blk, 0, s>>>(kp, 1);
+        for (int colour = 0; colour < 2; ++colour) {           // black, then red (ACMMP.cu:1549-1552)
+            if (kp.filt_hi[colour] <= kp.filt_lo[colour]) continue;
+            dim3 blk(64, 4), grd(cdiv(kp.Wh, 64), cdiv(kp.filt_hi[colour] - kp.filt_lo[colour], 4));
+            k_filter<<<grd, blk, 0, s>>>(kp, colour);
+        }
     }
     return hipGetLastError();
 }

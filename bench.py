@@ -237,6 +237,66 @@ def depth_exchange(args, ctx, rank, world, device, dist, allmax, reps=5):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+def band_split(args, rank, world, device, dist, allmax, reps=5):
+    """SURVEY.md §8e latency mode: the metric view (rank 0's scene on every rank) split into `world` row
+    bands, one per GPU, RunPatchMatch on each band with the 23-row halo swapped over RCCL after every
+    half-sweep (acmmp/band.py, acmmp_run_patchmatch_band).  Reports ms per depth map (band run + D2H of
+    the band's rows, max over ranks) against the same view on one GPU, and whether every band's rows
+    equal that whole-view run bit for bit.  A side measurement: never fails the bench."""
+    from acmmp import band
+    ctx = comm = None
+    try:
+        sc = make_scene(args, 0)
+        c0 = sc.cameras[0]
+        params = types.default_params(num_images=args.n_src + 1, max_iterations=args.iters,
+                                      depth_min=float(c0["depth_min"]) * 0.6, depth_max=float(c0["depth_max"]) * 1.2)
+        ctx = capi.Context(device)
+        ctx.set_math(args.math)
+        ctx.set_params(params)
+        ctx.upload_views(sc.images, sc.cameras)
+        uid = [capi.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = capi.Comm(device, uid[0], world, rank)
+        seed = args.seed + 900
+        ctx.run_patchmatch(seed)                                     # whole view on this GPU (reference)
+        whole_p, whole_c = ctx.download()
+        t1 = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ctx.run_patchmatch(seed)
+            ctx.download_into(whole_p, whole_c)
+            t1.append(time.perf_counter() - t0)
+        one_gpu_ms = allmax(float(np.median(t1))) * 1e3
+        lo, hi = band.run_rank(ctx, comm, seed, args.height, rank, world)     # warm-up + check
+        bp = np.empty((hi - lo, args.width, 4), np.float32)
+        bc = np.empty((hi - lo, args.width), np.float32)
+        ctx.download_rows_into(bp, bc, lo, hi)
+        same = (np.array_equal(bp.view(np.uint32), whole_p[lo:hi].view(np.uint32)) and
+                np.array_equal(bc.view(np.uint32), whole_c[lo:hi].view(np.uint32)))
+        same_all = allmax(0.0 if same else 1.0) == 0.0
+        tb = []
+        for _ in range(reps):
+            dist.barrier()
+            t0 = time.perf_counter()
+            band.run_rank(ctx, comm, seed, args.height, rank, world)
+            ctx.download_rows_into(bp, bc, lo, hi)
+            tb.append(allmax(time.perf_counter() - t0))
+        ms = float(np.median(tb)) * 1e3
+        return {"ranks": world, "bands": band.split_rows(args.height, world), "halo_rows": band.HALO,
+                "ms_per_depth_map": round(ms, 3), "one_gpu_ms_per_depth_map": round(one_gpu_ms, 3),
+                "speedup": round(one_gpu_ms / ms, 3), "bit_identical_to_whole_view": bool(same_all),
+                "exchanges_per_map": 2 * args.iters,
+                "transport": "RCCL grouped ncclSend/ncclRecv on the engine stream (acmmp_comm_band_exchange)",
+                "note": "one view split by rows over the GPUs; each rank downloads its own rows"}
+    except Exception as e:                                           # noqa: BLE001
+        return {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        if comm is not None:
+            comm.close()
+        if ctx is not None:
+            ctx.close()
+
+
 def pipeline_mode(args, rank, world, local_rank, barrier, allmax):
     """`--mode pipeline`: main.cpp's multi-scale ProcessProblem schedule (planar -> geom -> geom-multi,
     JBU, hierarchy planar -> geom -> geom-multi) over a synthetic multi-view capture in the ETH3D-style
@@ -459,6 +519,10 @@ def main():
     exch = None
     if world > 1 and ndev and world <= ndev and os.environ.get("ACMMP_BENCH_EXCHANGE", "1") != "0":
         exch = depth_exchange(args, ctx, rank, world, local_rank % ndev, dist, allmax)
+    # the single-view latency mode: one view's rows split over the GPUs
+    bsplit = None
+    if world > 1 and ndev and world <= ndev and os.environ.get("ACMMP_BENCH_BAND", "1") != "0":
+        bsplit = band_split(args, rank, world, local_rank % ndev, dist, allmax)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -507,6 +571,7 @@ def main():
             "nondegenerate_variant": variant,
             "end_to_end": e2e,
             "depth_exchange": exch,
+            "band_split": bsplit,
         }
         print(json.dumps(line), flush=True)
     ctx.close()

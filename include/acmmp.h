@@ -194,6 +194,31 @@ acmmp_status acmmp_last_work(const acmmp_ctx *ctx, unsigned long long *evaluated
  * environment variable ACMMP_TEX16=0 at upload time forces 4.  No reference counterpart. */
 int acmmp_texel_bytes(const acmmp_ctx *ctx);
 
+/* ---- row-band split of one reference view (SURVEY.md §8e latency mode; no reference counterpart:
+ * the reference runs a view on one GPU) -------------------------------------------------------------
+ * Several contexts (one per GPU) holding the same uploaded problem each run RunPatchMatch on the image
+ * rows [row0, row1) of one view; after every half-sweep each exchanges the updated colour's rows within
+ * ACMMP_BAND_HALO of its band with the neighbouring bands.  Each band's output rows are bit-identical to
+ * a whole-view acmmp_run_patchmatch with the same seed.  Bands must span >= ACMMP_BAND_HALO rows. */
+#define ACMMP_BAND_HALO 23
+
+/* RandomInitialization of the band +- halo (the same per-pixel values every band computes). */
+acmmp_status acmmp_band_begin(acmmp_ctx *ctx, uint64_t seed, int row0, int row1);
+/* The next half-sweep (black, red, black, ...) on the band's rows; *colour = the colour updated. */
+acmmp_status acmmp_band_sweep(acmmp_ctx *ctx, int *colour);
+/* Half-sweeps of the band run still to do (0 when none is in progress). */
+int acmmp_band_sweeps_left(const acmmp_ctx *ctx);
+/* Row ranges [a, b) of the halo exchange after a half-sweep: send to the band above, receive from it,
+ * send to the band below, receive from it (empty at the image edges).  A band's "send down" range is
+ * the next band's "receive from above" range and vice versa. */
+acmmp_status acmmp_band_halo_ranges(const acmmp_ctx *ctx, int ranges[8]);
+/* In-process exchange: copy rows [row_a, row_b) of `colour`'s current plane / cost / selected-view
+ * state from src to dst (same or peer device; waits for src's stream). */
+acmmp_status acmmp_band_copy_rows(acmmp_ctx *dst, acmmp_ctx *src, int colour, int row_a, int row_b);
+/* GetDepthandNormal + the two filters on band +- 10 / 5 rows; synchronous.  Rows [row0, row1) of the
+ * row-major outputs (acmmp_download / acmmp_device_outputs) are then final. */
+acmmp_status acmmp_band_end(acmmp_ctx *ctx, int do_post);
+
 /* ---- device buffers and the multi-GPU communicator (no reference counterpart:
  * the reference is single-GPU and exchanges depth maps through dmb files) ------------------- */
 
@@ -216,6 +241,16 @@ acmmp_status acmmp_comm_broadcast(acmmp_comm *comm, int n, void *const *bufs, co
 
 /* Element-wise max over ranks of n host doubles (timing reductions); synchronous. */
 acmmp_status acmmp_comm_allreduce_max(acmmp_comm *comm, double *vals, int n);
+
+/* Halo exchange of a band run over RCCL: after acmmp_band_sweep updated `colour`, grouped ncclSend /
+ * ncclRecv of the acmmp_band_halo_ranges rows with rank_up / rank_down (-1 = none), queued on the
+ * context's stream (ordered with its kernels, no host wait). */
+acmmp_status acmmp_comm_band_exchange(acmmp_comm *comm, acmmp_ctx *ctx, int colour, int rank_up, int rank_down);
+
+/* A whole band run: begin, every half-sweep followed by the RCCL halo exchange, end.  comm may be
+ * NULL for a single band covering the view.  Synchronous on return. */
+acmmp_status acmmp_run_patchmatch_band(acmmp_ctx *ctx, acmmp_comm *comm, uint64_t seed, int row0, int row1,
+                                       int rank_up, int rank_down);
 
 /* ---- GPU depth-map fusion (RunFusionCuda + SimpleFusionKernel, ACMMP.cu:1662-2105) -------------
  * One object per fusion run.  cams[i] is view i's camera already rescaled to its depth map
