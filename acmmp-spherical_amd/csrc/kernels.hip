@@ -397,6 +397,8 @@ struct Patch {
     const float4* rw;               // [s * stride] = (ray.x, ray.y, ray.z, w); null when not staged
     const float* rr;                // [s * stride] = reference texel
     const float2* wr;               // lite staging: [s * stride] = (w, texel); rays re-read from the tables
+    const float2* row;              // separable SPHERE staging (STAGED 4): (sin, cos) latitude per patch row
+    const float2* col;              //   and (sin, cos) longitude per patch column; wr holds (w, texel)
     int stride;
     float center;                   // reference texel at the pixel
     float sbw, sref, srr;
@@ -617,7 +619,7 @@ template <int MODEL>
 __device__ __forceinline__ Patch make_patch(const KParams& kp, int px, int py) {
     const DevCam& rc = kp.cams[0];
     Patch pt;
-    pt.rw = nullptr; pt.rr = nullptr; pt.wr = nullptr; pt.stride = 0;
+    pt.rw = nullptr; pt.rr = nullptr; pt.wr = nullptr; pt.row = pt.col = nullptr; pt.stride = 0;
     pt.center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
     patch_sums<MODEL>(kp, pt, px, py);
     return pt;
@@ -684,13 +686,19 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     }
     const int R = kp.R, inc = kp.inc;
     constexpr int G = PIPE ? VB : (TEX == 1 ? kPipeG16 : kPipeG);
-    int s = 0;
-    for (int i = -R; i <= R; i += inc) {
+    int s = 0, ii = 0;
+    for (int i = -R; i <= R; i += inc, ++ii) {
         int jj = 0;                                      // s % nside without a division per sample
+        const float2 cs = STAGED == 4 ? pt.col[ii] : make_float2(0.f, 0.f);
         for (int j = -R; j <= R; j += inc, ++s, ++jj) {
             float r;
             float4 rw;
-            if (STAGED == 1) {
+            if (STAGED == 4) {                           // coop_patch_sep layout (SPHERE): ray_at's products
+                const float2 rs = pt.row[jj];
+                const float2 q = pt.wr[s];
+                rw = make_float4(rs.y * cs.x, -rs.x, rs.y * cs.y, q.x);
+                r = q.y;
+            } else if (STAGED == 1) {
                 rw = pt.rw[s * pt.stride];
                 r = pt.rr[s * pt.stride];
             } else if (STAGED == 3) {                    // coop_patch_nb layout
@@ -1384,7 +1392,7 @@ __device__ __forceinline__ Patch coop_patch(const KParams& kp, bool valid, int p
     }
     __syncthreads();
     Patch pt;
-    pt.rw = rw; pt.rr = rr; pt.wr = nullptr; pt.stride = 1;
+    pt.rw = rw; pt.rr = rr; pt.wr = nullptr; pt.row = pt.col = nullptr; pt.stride = 1;
     pt.center = 0.f;
     // every lane of the pixel sums its SPHERE weights itself (same order, same bits): no LDS slot
     // and no second barrier, which keeps k_eval_nb's block at 20160 B of LDS (8 blocks per CU)
@@ -1442,12 +1450,55 @@ __device__ __forceinline__ Patch coop_patch_nb(const KParams& kp, bool valid, in
     }
     __syncthreads();
     Patch pt;
-    pt.rw = rw; pt.rr = rr; pt.wr = nullptr; pt.stride = 1;
+    pt.rw = rw; pt.rr = rr; pt.wr = nullptr; pt.row = pt.col = nullptr; pt.stride = 1;
     pt.center = 0.f;
     pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f;
     if (MODEL == kSphere && valid) {
         for (int s = 0; s < kp.S; ++s) {                // patch_sums order (ACMMP.cu:482-486)
             const float w = rw[s].z, r = rw[s].w;
+            pt.sbw += w;
+            pt.sref = fmaf(w, r, pt.sref);
+            pt.srr = fmaf(w * r, r, pt.srr);
+        }
+    }
+    return pt;
+}
+
+// Separable SPHERE staging (STAGED 4): (w, texel) per sample, (sin, cos) of the latitude per patch row
+// and of the longitude per patch column -- a sample's ray is ray_at's two products of them, the same
+// bits.  8 S + 16 nside bytes per pixel (384 B at 36 samples, vs 600 B for coop_patch_nb), so
+// k_eval_ref's 51-pixel block fits 8 times in a CU's LDS instead of 5.
+static inline size_t sep_lds_bytes(int S, int nside, int npix) { return (8 * static_cast<size_t>(S) + 16 * nside) * npix; }
+
+template <int NPIX, int NLANES>
+__device__ __forceinline__ Patch coop_patch_sep(const KParams& kp, bool valid, int px, int py, int lp, int h,
+                                                float4* lds) {
+    float2* base = reinterpret_cast<float2*>(lds);
+    float2* wr = base + lp * kp.S;
+    float2* row = base + NPIX * kp.S + lp * 2 * kp.nside;
+    float2* col = row + kp.nside;
+    if (valid) {
+        const DevCam& rc = kp.cams[0];
+        const float center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
+        for (int s = h; s < kp.S; s += NLANES) {
+            const int i = -kp.R + (s / kp.nside) * kp.inc, j = -kp.R + (s % kp.nside) * kp.inc;
+            float r;
+            const float4 q = patch_sample<kSphere>(kp, px, py, s, i, j, center, r);
+            wr[s] = make_float2(q.w, r);
+        }
+        for (int k = h; k < kp.nside; k += NLANES) {
+            row[k] = kp.sph_row[py - kp.R + k * kp.inc + kp.R];
+            col[k] = kp.sph_col[px - kp.R + k * kp.inc + kp.R];
+        }
+    }
+    __syncthreads();
+    Patch pt;
+    pt.rw = nullptr; pt.rr = nullptr; pt.wr = wr; pt.row = row; pt.col = col; pt.stride = 1;
+    pt.center = 0.f;
+    pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f;
+    if (valid) {
+        for (int s = 0; s < kp.S; ++s) {                // patch_sums order (ACMMP.cu:482-486)
+            const float w = wr[s].x, r = wr[s].y;
             pt.sbw += w;
             pt.sref = fmaf(w, r, pt.sref);
             pt.srr = fmaf(w * r, r, pt.srr);
@@ -1473,7 +1524,7 @@ __device__ __forceinline__ Patch coop_patch_lite(const KParams& kp, bool valid, 
     }
     __syncthreads();
     Patch pt;
-    pt.rw = nullptr; pt.rr = nullptr; pt.wr = wr; pt.stride = 1;
+    pt.rw = nullptr; pt.rr = nullptr; pt.wr = wr; pt.row = pt.col = nullptr; pt.stride = 1;
     pt.center = 0.f;
     if (valid) patch_sums<MODEL>(kp, pt);
     else { pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f; }
@@ -1492,6 +1543,9 @@ __device__ __forceinline__ Patch coop_patch_lite(const KParams& kp, bool valid, 
 #ifndef ACMMP_REF_LITE
 #define ACMMP_REF_LITE 0                    // k_eval_ref: 1 = (w, texel) staging, rays re-read from the tables
 #endif
+#ifndef ACMMP_REF_SEP
+#define ACMMP_REF_SEP 1                     // k_eval_ref (SPHERE, V <= 4): separable staging, 8 blocks per CU instead of 5
+#endif                                      // (r02 A/B: metric +0.8%, exact +0.9%; V = 15 -0.5%, so not there)
 #ifndef ACMMP_REF_VBA
 #define ACMMP_REF_VBA 2                     // k_eval_ref / tail: 2-view NCC chunks where launches have 4-view ones (r01_v40 A/B +1.7%)
 #endif
@@ -1915,8 +1969,10 @@ __global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_
     constexpr int kStaged = 2;
     const Patch pt = coop_patch_lite<MODEL>(kp, valid, px, py, lp, h, kRefLanes, reinterpret_cast<float2*>(lds4));
 #else
-    constexpr int kStaged = 3;
-    const Patch pt = coop_patch_nb<MODEL, kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
+    constexpr int kStaged = (MODEL == kSphere && ACMMP_REF_SEP && VB <= 4) ? 4 : 3;
+    Patch pt;
+    if constexpr (kStaged == 4) pt = coop_patch_sep<kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
+    else pt = coop_patch_nb<MODEL, kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
 #endif
     constexpr int VBA = (VB == 4 && ACMMP_REF_VBA == 2) ? 2 : (VB > kEvalVB ? kEvalVB : VB);
     if (!valid) return;
@@ -1997,7 +2053,7 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
         const float4 tp = kp.cand[h * Pc + ci];
         Patch pt;                                            // make_patch's values, from k_eval_ref
         const float4 ps = kp.psum[ci];
-        pt.rw = nullptr; pt.rr = nullptr; pt.wr = nullptr; pt.stride = 0;
+        pt.rw = nullptr; pt.rr = nullptr; pt.wr = nullptr; pt.row = pt.col = nullptr; pt.stride = 0;
         pt.sbw = ps.x; pt.sref = ps.y; pt.srr = ps.z; pt.center = ps.w;
         float temp_cost = kp.cand_cost[h * Pc + ci];
         float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
@@ -2366,7 +2422,9 @@ hipError_t launch_select(const KParams& kp, int colour, int iter, hipStream_t s)
 #if ACMMP_IN_TU(4)
 hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s) {
     const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
-    const size_t lds_ref = ACMMP_REF_LITE ? sizeof(float2) * kp.S * kRefPix : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
+    const size_t lds_ref = ACMMP_REF_LITE ? sizeof(float2) * kp.S * kRefPix
+                         : (kp.model == kSphere && ACMMP_REF_SEP && pick_vb(kp.V) <= 4) ? sep_lds_bytes(kp.S, kp.nside, kRefPix)
+                                                                 : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
     hipError_t e = hipSuccess;
     if (kp.ref_split > 0 && (e = hipMemsetAsync(kp.surv_count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
     const dim3 grd_ref = eval_grid(cdiv(npix, kRefPix));
