@@ -270,7 +270,9 @@ class ViewStore:
         self.shapes = {}                             # (key, view) -> (H, W)
 
     def put(self, key, view, arr, ctx=None):
-        arr = np.ascontiguousarray(arr, np.float32)
+        # float32 views are kept as they are (a depth or normals slice of the downloaded planes costs no
+        # copy here; consumers that need contiguous memory make it when they do)
+        arr = np.asarray(arr, np.float32)
         self.host[(key, view)] = arr
         self.shapes[(key, view)] = arr.shape
         if self.device is not None and key in ("depths", "depths_geom"):
@@ -514,8 +516,8 @@ class Pipeline:
                 planes, costs = e.download()
         with self._timed("store"):
             key = "depths_geom" if geom else "depths"
-            self._save(key, ref, planes[..., 3].copy(), e if isinstance(e, capi.Context) else None)
-            self.store.put("normals", ref, planes[..., :3].copy())
+            self._save(key, ref, planes[..., 3], e if isinstance(e, capi.Context) else None)
+            self.store.put("normals", ref, planes[..., :3])
             self.store.put("costs", ref, costs)
             self._last_planes[ref] = planes
             if self.out_folder:
