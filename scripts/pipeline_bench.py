@@ -27,10 +27,12 @@ def main():
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--model", choices=["sphere", "pinhole"], default="sphere")
     ap.add_argument("--n-src", type=int, default=0, help="sources per view (nearest camera centres); 0 = all")
+    ap.add_argument("--math", choices=["exact", "fast"], default="exact", help="engine arithmetic (acmmp_set_math)")
+    ap.add_argument("--n-waves", type=int, default=48, help="texture waves of the synthetic scene (fewer = faster to render)")
     a = ap.parse_args()
     make = scene.sphere_scene if a.model == "sphere" else scene.pinhole_scene
     t_scene = time.perf_counter()
-    sc = make(a.width, a.height, n_src=a.views - 1, seed=a.seed)
+    sc = make(a.width, a.height, n_src=a.views - 1, seed=a.seed, n_waves=a.n_waves)
     print(f"scene: {a.views} views {a.width}x{a.height} {a.model} in {time.perf_counter() - t_scene:.1f} s", flush=True)
     centres = np.array([-(np.asarray(c["R"], np.float64).reshape(3, 3).T @ np.asarray(c["t"], np.float64))
                         for c in sc.cameras])
@@ -55,11 +57,11 @@ def main():
         print(msg, flush=True)
 
     t0 = time.perf_counter()
-    pipe = pipeline.Pipeline(ds, order="reference", log=log).run()
+    pipe = pipeline.Pipeline(ds, order="reference", log=log, math=a.math).run()
     total = time.perf_counter() - t0
     d0 = pipe.store.get("depths_geom", 0)
     acc = scene.depth_accuracy(d0, sc.gt_depth) if d0.shape == sc.gt_depth.shape else None
-    print(json.dumps({"views": a.views, "size": [a.width, a.height], "model": a.model,
+    print(json.dumps({"views": a.views, "size": [a.width, a.height], "model": a.model, "math": a.math,
                       "n_src": len(problems[0].src_image_ids), "passes": [p.name for p in pipe.passes],
                       "total_s": round(total, 3), "s_per_view_pass": round(total / (a.views * len(pipe.passes)), 4),
                       "pass_s": [round(t, 3) for _, t in times[1:]] + [round(time.perf_counter() - last[0], 3)],
