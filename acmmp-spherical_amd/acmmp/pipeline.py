@@ -27,7 +27,9 @@ import contextlib
 import copy
 import math
 import os
+import threading
 import time
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -321,7 +323,7 @@ class Pipeline:
     def __init__(self, ds: Dataset, engine=None, exchange=None, device: int = 0, seed: int = 1234,
                  order: str = "reference", geom_iterations: int = 2, out_folder: str | None = None,
                  use_device_store: bool | None = None, size_bound: int = 1000, max_image_size: int = 3200,
-                 log=None, reuse_planes: bool = True, math: str | None = None):
+                 log=None, reuse_planes: bool = True, math: str | None = None, overlap: bool = True):
         self.ds = ds
         # a geom pass restarts from the previous pass's depth + normals of its view, which is that
         # pass's downloaded plane array: keep it instead of re-joining the two stored maps
@@ -352,6 +354,12 @@ class Pipeline:
         self.passes = []
         self._pending = []
         self.stage_s = {}                                   # host wall seconds per stage (profiling)
+        self._stage_lock = threading.Lock()
+        # planar passes: overlap a view's host planar-prior block with the next view's first
+        # RunPatchMatch (second engine context on the same GPU, one worker thread; _pass_overlapped)
+        self.overlap = overlap and gpu
+        self._engine2 = None
+        self._math = math
 
     @contextlib.contextmanager
     def _timed(self, stage):
@@ -359,7 +367,16 @@ class Pipeline:
         try:
             yield
         finally:
-            self.stage_s[stage] = self.stage_s.get(stage, 0.0) + time.perf_counter() - t0
+            dt = time.perf_counter() - t0
+            with self._stage_lock:
+                self.stage_s[stage] = self.stage_s.get(stage, 0.0) + dt
+
+    def close(self):
+        """Release the engine context(s) this pipeline created or was given."""
+        for e in (self._engine2, self.engine):
+            if e is not None and hasattr(e, "close"):
+                e.close()
+        self._engine2 = None
 
     # -- sharding
     def owner(self, i: int) -> int:
@@ -397,9 +414,12 @@ class Pipeline:
         self.log(f"[rank {self.rank}] pass {self.pass_index}: {name}")
         log = PassLog(name)
         t0 = time.perf_counter()
-        for i in self.my_problems():
-            self.process_problem(i, geom, planar, hier, multi)
-            log.views.append(self.problems[i].ref_image_id)
+        if planar and not geom and self.overlap and len(self.my_problems()) > 1:
+            self._pass_overlapped(hier, log)
+        else:
+            for i in self.my_problems():
+                self.process_problem(i, geom, planar, hier, multi)
+                log.views.append(self.problems[i].ref_image_id)
         self._commit_pending()
         log.compute_s = time.perf_counter() - t0
         key = "depths_geom" if geom else "depths"
@@ -472,8 +492,35 @@ class Pipeline:
             bufs.append(b)
         e.upload_views_device(bufs, cams)
 
+    def _pass_overlapped(self, hier, log):
+        """A planar pass with two engine contexts on the GPU: view k's second half (host planar prior,
+        second RunPatchMatch, store) runs on a worker thread while the main thread runs view k+1's
+        first half on the other context.  The views of a planar pass are independent (each reads only
+        its own view's earlier-pass state), so the outputs are those of the sequential loop."""
+        if self._engine2 is None:
+            self._engine2 = capi.Context(self.device)
+            if self._math is not None:
+                self._engine2.set_math(self._math)
+        engines = [self.engine, self._engine2]
+        busy = [None, None]
+        with ThreadPoolExecutor(1) as pool:
+            for k, i in enumerate(self.my_problems()):
+                slot = k % 2
+                if busy[slot] is not None:
+                    busy[slot].result()                      # the context is free again
+                head = self._problem_head(i, False, True, hier, False, engines[slot])
+                busy[slot] = pool.submit(self._problem_tail, head)
+                log.views.append(self.problems[i].ref_image_id)
+            for f in busy:
+                if f is not None:
+                    f.result()
+
     # -- ProcessProblem (main.cpp:73-210)
     def process_problem(self, idx, geom, planar, hier, multi):
+        return self._problem_tail(self._problem_head(idx, geom, planar, hier, multi, self.engine))
+
+    def _problem_head(self, idx, geom, planar, hier, multi, e):
+        """InuputInitialization, CudaSpaceInitialization and the first RunPatchMatch of ProcessProblem."""
         prob = self.problems[idx]
         ref = prob.ref_image_id
         with self._timed("inputs"):
@@ -489,7 +536,6 @@ class Pipeline:
             p["multi_geometry"] = int(multi)
         if hier:
             p["hierarchy"] = 1
-        e = self.engine
         H, W = images[0].shape
         with self._timed("upload"):
             self._upload(e, p, images, cams, ids, ref, geom, hier, H, W)
@@ -497,6 +543,12 @@ class Pipeline:
         with self._timed("patchmatch"):
             e.run_patchmatch(run_seed)
             planes, costs = e.download()
+        return dict(e=e, p=p, c0=c0, ref=ref, geom=geom, planar=planar, run_seed=run_seed, planes=planes, costs=costs)
+
+    def _problem_tail(self, st):
+        """The planar block (main.cpp:113-187) with its second RunPatchMatch, and the stores."""
+        e, p, c0, ref, geom, planar, run_seed = (st[k] for k in ("e", "p", "c0", "ref", "geom", "planar", "run_seed"))
+        planes, costs = st["planes"], st["costs"]
         if planar:                                                   # main.cpp:113-187
             p["planar_prior"] = 1
             if hasattr(e, "set_planar_prior_from_maps"):

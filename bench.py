@@ -115,7 +115,7 @@ def end_to_end(args, sc, device):
     t0 = time.perf_counter()
     pipe.run()
     total = time.perf_counter() - t0
-    pipe.engine.close()
+    pipe.close()
     d0 = pipe.store.get("depths_geom", 0)
     acc = scene.depth_accuracy(d0, sc.gt_depth) if d0.shape == sc.gt_depth.shape else None
     return {"views": n, "passes": [p.name for p in pipe.passes], "total_s": round(total, 3),
@@ -357,7 +357,7 @@ def pipeline_mode(args, rank, world, local_rank, barrier, allmax):
         "quality": {"view0_frac_within_1pct_gt": round(float(acc[0]), 4) if acc else None},
     }
     exchange.close()
-    pipe.engine.close()
+    pipe.close()
     return line
 
 
