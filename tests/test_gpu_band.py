@@ -28,7 +28,7 @@ def _scene(kind, W, H, V, seed):
     return scene.sphere_scene(W, H, n_src=V, seed=seed)
 
 
-def _setup(ctx, sc, p, math, depths=None, state=None):
+def _setup(ctx, sc, p, math, depths=None, state=None, scaled=None, prior=None):
     ctx.set_math(math)
     ctx.set_params(p)
     ctx.upload_views(sc.images, sc.cameras)
@@ -36,6 +36,10 @@ def _setup(ctx, sc, p, math, depths=None, state=None):
         ctx.upload_depths(depths)
     if state is not None:
         ctx.set_state(*state)
+    if scaled is not None:
+        ctx.set_scaled_state(scaled)
+    if prior is not None:
+        ctx.set_planar_prior(*prior)
 
 
 def _outputs(ctx):
@@ -44,18 +48,18 @@ def _outputs(ctx):
     return planes, costs, sel
 
 
-def _compare_bands(sc, p, math, nbands, seed, depths=None, state=None, do_post=True):
+def _compare_bands(sc, p, math, nbands, seed, depths=None, state=None, do_post=True, scaled=None, prior=None):
     H = sc.images[0].shape[0]
     full = capi.Context(0)
     ctxs = [capi.Context(0) for _ in range(nbands)]
     try:
-        _setup(full, sc, p, math, depths, state)
+        _setup(full, sc, p, math, depths, state, scaled, prior)
         full.run_patchmatch(seed, do_post=do_post)
         want = _outputs(full)
         bands = band.split_rows(H, nbands)
         assert len(bands) == nbands
         for ctx in ctxs:
-            _setup(ctx, sc, p, math, depths, state)
+            _setup(ctx, sc, p, math, depths, state, scaled, prior)
         band.run_local(ctxs, seed, bands, do_post=do_post)
         for ctx, (lo, hi) in zip(ctxs, bands):
             got = _outputs(ctx)
@@ -94,6 +98,43 @@ def test_bands_geom_pass(kind):
     costs0 = rng.uniform(0, 1, (H, W)).astype(np.float32)
     p = _params(sc, geom_consistency=1, max_iterations=2)
     _compare_bands(sc, p, "exact", 2, seed=7, depths=depths, state=(st, costs0))
+
+
+def test_bands_hierarchy_upsample():
+    """The upsample init branch (ACMMP.cu:713-779: JBU of the coarse normals around each pixel, pre_costs)
+    and the hierarchy gate, split in three bands."""
+    sc = _scene("sphere", 96, 72, 2, seed=51)
+    H, W, h, w = 72, 96, 36, 48
+    rng = np.random.default_rng(4)
+    coarse = np.zeros((h, w, 4), np.float32)
+    coarse[..., :3] = rng.normal(0, 0.2, (h, w, 3))
+    coarse[..., 2] -= 1.0
+    coarse[..., :3] /= np.linalg.norm(coarse[..., :3], axis=-1, keepdims=True)
+    coarse[..., 3] = rng.uniform(0.05, 1.5, (h, w))
+    cur = np.zeros((H, W, 4), np.float32)
+    cur[..., 3] = (sc.gt_depth * rng.uniform(0.95, 1.05, (H, W))).astype(np.float32)
+    p = _params(sc, hierarchy=1, upsample=1, scaled_cols=w, scaled_rows=h)
+    _compare_bands(sc, p, "exact", 3, seed=9, state=(cur, None), scaled=coarse)
+
+
+@pytest.mark.parametrize("math,geom", [("exact", 0), ("fast", 0), ("exact", 1)])
+def test_bands_planar_prior(math, geom):
+    """Prior-restricted propagation / refinement, with geom the planar-prior init branch too
+    (ACMMP.cu:690-711), split in two bands."""
+    sc = _scene("pinhole", 88, 60, 2, seed=41)
+    H, W = sc.images[0].shape
+    rng = np.random.default_rng(2)
+    prior = np.zeros((H, W, 4), np.float32)
+    prior[..., 2] = -1.0
+    prior[..., 3] = (sc.gt_depth * rng.uniform(0.95, 1.05, (H, W))).astype(np.float32)
+    masks = (rng.uniform(0, 1, (H, W)) < 0.6).astype(np.uint32) * rng.integers(1, 50, (H, W)).astype(np.uint32)
+    st = np.zeros((H, W, 4), np.float32)
+    st[..., 2] = -1.0
+    st[..., 3] = sc.gt_depth
+    costs0 = rng.uniform(0, 1, (H, W)).astype(np.float32)
+    depths = [(sc.gt_depth * np.float32(1.01)).astype(np.float32)] * 3 if geom else None
+    p = _params(sc, planar_prior=1, geom_consistency=geom, max_iterations=2 if geom else 3)
+    _compare_bands(sc, p, math, 2, seed=5, depths=depths, state=(st, costs0), prior=(prior, masks))
 
 
 def test_single_band_rccl_entry_equals_run():
