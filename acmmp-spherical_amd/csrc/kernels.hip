@@ -1546,6 +1546,9 @@ __device__ __forceinline__ Patch coop_patch_lite(const KParams& kp, bool valid, 
 #ifndef ACMMP_REF_SEP
 #define ACMMP_REF_SEP 1                     // k_eval_ref (SPHERE, V <= 4): separable staging, 8 blocks per CU instead of 5
 #endif                                      // (r02 A/B: metric +0.8%, exact +0.9%; V = 15 -0.5%, so not there)
+#ifndef ACMMP_REF_VBA_WIDE
+#define ACMMP_REF_VBA_WIDE 1                // SPHERE: 2-view chunks for V > 4 launches too (r02 A/B: V = 15 +1.4%,
+#endif                                      // k_eval_ref -5%; pinhole V = 10 -4%, so SPHERE only)
 #ifndef ACMMP_REF_VBA
 #define ACMMP_REF_VBA 2                     // k_eval_ref / tail: 2-view NCC chunks where launches have 4-view ones (r01_v40 A/B +1.7%)
 #endif
@@ -1974,7 +1977,7 @@ __global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_
     if constexpr (kStaged == 4) pt = coop_patch_sep<kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
     else pt = coop_patch_nb<MODEL, kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
 #endif
-    constexpr int VBA = (VB == 4 && ACMMP_REF_VBA == 2) ? 2 : (VB > kEvalVB ? kEvalVB : VB);
+    constexpr int VBA = ((VB == 4 || (VB > 4 && MODEL == kSphere && ACMMP_REF_VBA_WIDE)) && ACMMP_REF_VBA == 2) ? 2 : (VB > kEvalVB ? kEvalVB : VB);
     if (!valid) return;
     if (kp.ref_split > 0 && h == 0) {                        // the tail's patch, without re-summing it
         const DevCam& rc = kp.cams[0];
@@ -2057,7 +2060,7 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
         pt.sbw = ps.x; pt.sref = ps.y; pt.srr = ps.z; pt.center = ps.w;
         float temp_cost = kp.cand_cost[h * Pc + ci];
         float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
-        constexpr int VBT = (VB == 4 && ACMMP_REF_VBA == 2) ? 2 : (VB > kEvalVB ? kEvalVB : VB);
+        constexpr int VBT = ((VB == 4 || (VB > 4 && MODEL == kSphere && ACMMP_REF_VBA_WIDE)) && ACMMP_REF_VBA == 2) ? 2 : (VB > kEvalVB ? kEvalVB : VB);
         for_all_views_tf<MODEL, VBT, 0, ACMMP_REF_PIPE, TF>(kp, px, py, pt, tp, umask, [&](int v, float c) {
             vcost[v * Pc] = c;
             const float w = vw_get(vwp, v);
