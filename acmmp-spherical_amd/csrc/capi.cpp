@@ -702,6 +702,8 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.ref_split = ref_split_point(kp.V, Pc);
     if (!c->d_work) HIP_TRY(c, dalloc(c->d_work, 256));
     kp.work = c->d_work;
+    kp.nb_views = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
+    kp.nb_count_work = 1;
     return ACMMP_OK;
 }
 

@@ -119,6 +119,8 @@ struct KParams {
     float* cand_cost;               // [5][Pc] their aggregated costs
     PixState* pst;                  // [Pc]
     unsigned long long* work;       // [256] k_eval_nb pixels with NCC work (SPHERE patch sum >= 1e-6), per block % 256
+    uint32_t nb_views;              // k_eval_nb: the source views this launch evaluates (all, or a chunk of them)
+    int nb_count_work;              // k_eval_nb: this launch adds to `work` (the first launch of a half-sweep)
     long long Pc;                   // H * Wh
     // split refinement: k_eval_ref evaluates views [0, ref_split) of every candidate,
     // drops the ones whose partial aggregate already cannot beat cost_now, and queues the rest

@@ -17,6 +17,7 @@
 //  * current-hypothesis and refinement costs are evaluated only for views some
 //    lane of the wave selected (zero-weight views add exactly +0 in the reference).
 #include <algorithm>
+#include <cstdlib>
 
 #include "detmath.h"
 #include "engine.h"
@@ -1573,6 +1574,9 @@ __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour
 
 #endif  // ACMMP_IN_TU(0)
 
+#ifndef ACMMP_NB_VIEW_CHUNK_DEFAULT
+#define ACMMP_NB_VIEW_CHUNK_DEFAULT 0       // views per k_eval_nb launch (0 = all in one launch)
+#endif
 #ifndef ACMMP_NB_WAVES
 #define ACMMP_NB_WAVES 8                    // k_eval_nb (SPHERE): minimum waves per SIMD the register budget must allow
 #endif
@@ -1595,7 +1599,7 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_WAVES_FM : A
     const Patch pt = coop_patch_nb<MODEL>(kp, valid, px, py, lp, h, lds4);
     // work accounting for the roofline: pixels whose NCCs are evaluated (not short-circuited)
     const int busy = __syncthreads_count(valid && h == 0 && !(MODEL == kSphere && pt.sbw < 1e-6f));
-    if (t == 0 && busy) atomicAdd(kp.work + (blockIdx.x & 255u), static_cast<unsigned long long>(busy));
+    if (t == 0 && busy && kp.nb_count_work) atomicAdd(kp.work + (blockIdx.x & 255u), static_cast<unsigned long long>(busy));
     if (!valid) return;
     const long long Pc = kp.Pc;
     const long long ci = static_cast<long long>(py) * kp.Wh + (px >> 1);
@@ -1607,7 +1611,7 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_WAVES_FM : A
 #endif
     if (pos < 0) return;
     const float4 ph = plane_at(kp, pos);
-    const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
+    const uint32_t all = kp.nb_views;
     float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
     for_all_views_t<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, FM ? ACMMP_NB_PIPE_FAST : ACMMP_NB_PIPE, TEX, FM>(
         kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
@@ -2394,11 +2398,42 @@ hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, cons
 // The half-sweep's launches, each in its own translation unit (their kernels are the bulk of the
 // template instances); launch_propagate strings them together.
 hipError_t launch_eval_nb(const KParams& kp, int colour, hipStream_t s);
+hipError_t launch_eval_nb_views(const KParams& kp, int colour, hipStream_t s);
 hipError_t launch_select(const KParams& kp, int colour, int iter, hipStream_t s);
 hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s);
 
 #if ACMMP_IN_TU(2)
-hipError_t launch_eval_nb(const KParams& kp, int colour, hipStream_t s) {
+// View-chunked k_eval_nb: one launch per chunk of 8 source views when the sources' texels outgrow the
+// 256 MB Infinity Cache, so all waves in flight sample the same few images (r02 A/B
+// profiles/r02_view_chunk_ab.txt: SPHERE V = 15 at 3200x1600 +3.7%, at 4096x2048 +6.4%; pinhole V = 10
+// at 1600x1200, 77 MB of texels, -1% -- not chunked).  ACMMP_NB_VIEW_CHUNK=c overrides (c <= 0: one
+// launch over all views); read per half-sweep.
+static int nb_view_chunk(const KParams& kp) {
+    const char* e = std::getenv("ACMMP_NB_VIEW_CHUNK");
+    int c = e ? std::atoi(e) : ACMMP_NB_VIEW_CHUNK_DEFAULT;
+    if (!e && c == 0) {
+        // texel bytes of the sources at the reference's size (row-pair binary16 or fp32: 4 B per texel)
+        const double bytes = 4.0 * (kp.W + 2) * (kp.H + 2) * kp.V;
+        c = (kp.V > 8 && bytes > 160e6) ? 8 : 0;
+    }
+    return (c <= 0 || c >= kp.V) ? kp.V : c;
+}
+
+hipError_t launch_eval_nb(const KParams& kp0, int colour, hipStream_t s) {
+    KParams kp = kp0;
+    const int chunk = nb_view_chunk(kp);
+    for (int v0 = 0; v0 < kp.V; v0 += chunk) {
+        const int v1 = std::min(kp.V, v0 + chunk);
+        const uint32_t hi = v1 >= 32 ? 0xFFFFFFFFu : ((1u << v1) - 1u);
+        kp.nb_views = hi & ~((1u << v0) - 1u);
+        kp.nb_count_work = v0 == 0;
+        const hipError_t e = launch_eval_nb_views(kp, colour, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_eval_nb_views(const KParams& kp, int colour, hipStream_t s) {
     const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
     const size_t lds_nb = nb_lds_bytes(kp.model, kp.S, kp.nside);
     const dim3 grd = eval_grid(cdiv(npix, kNbPix));

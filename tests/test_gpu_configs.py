@@ -81,6 +81,18 @@ def test_many_views_full_run_bitexact(ctx, oracle_mod, kind, W, H, V):
         assert np.any(g["selected_views"] >> 16)
 
 
+@pytest.mark.parametrize("kind,V,chunk", [("sphere", 15, "8"), ("pinhole", 20, "3"), ("sphere", 32, "8")])
+def test_view_chunked_neighbour_eval_bitexact(ctx, oracle_mod, monkeypatch, kind, V, chunk):
+    """k_eval_nb in view-chunked launches (ACMMP_NB_VIEW_CHUNK; chosen automatically when the sources'
+    texels outgrow the Infinity Cache, e.g. C3's 15 views at 4096x2048): the same bits as one launch."""
+    sc = make(kind, 48, 24 if kind == "sphere" else 36, V, seed=V + 11)
+    p = params_for(sc)
+    monkeypatch.setenv("ACMMP_NB_VIEW_CHUNK", chunk)
+    g = gpu_full(ctx, sc, p, seed=77)
+    o = oracle_mod.run_patchmatch(oracle_mod.Problem(sc.images, sc.cameras, p), seed=77, nthreads=16)
+    check(g, o)
+
+
 @pytest.mark.parametrize("V", [10, 20])
 def test_many_views_geom_pass_bitexact(ctx, oracle_mod, V):
     """C2's geometric-consistency pass (ACMMP.cpp:653-678, 726-786; max_iterations = 2) with V
