@@ -1759,7 +1759,10 @@ __global__ __launch_bounds__(256, ACMMP_SEL_WAVES) void k_select(const KParams k
             for (int j = 0; j < VMAX; ++j)
                 if (j < V) add_view(j, ca[i][j]);
         } else {
-            for (int j = 0; j < V; ++j) add_view(j, cost_arr(i, j));
+            // only the selected views' costs are read (a zero-weight view adds nothing): at V = 15 about
+            // a quarter of the 8 x V matrix, which k_eval_nb's slab holds in HBM at C3 sizes
+            for (int j = 0; j < V; ++j)
+                if ((temp_sel >> j) & 1u) add_view(j, cost_arr(i, j));
         }
         final_costs[i] = fc / weight_norm;
     }
