@@ -1150,11 +1150,12 @@ __device__ __forceinline__ float range_gauss(float x, float sigma) {
 // the common random branch does not carry the JBU loop's registers.
 enum InitBranch { kInitRandom = 0, kInitPlanar = 1, kInitUpsample = 2, kInitReuse = 3 };
 
-// k_init evaluates its (unstaged) NCCs two views at a time: with one lane per pixel every lane gathers
-// its own samples, and a wider chunk multiplies the wave's texel footprint past L1/L2 (measured: 1 view
-// 1.55 ms, 2 views 1.36 ms, 4 views 1.41 ms at 2000x1500, V = 4).
+// k_init evaluates its (unstaged) NCCs four views at a time: each chunk recomputes the samples' weights
+// and rays, and with the fast-math projection the wider chunk wins (r02 A/B profiles/r02_init_vb_ab.txt:
+// 2 -> 4 views: 0.95 -> 0.92 ms at the metric, 2.46 -> 2.15 ms at C2, 8.27 -> 6.97 ms at C3; round 1,
+// exact mode only: 1 view 1.55, 2 views 1.36, 4 views 1.41 ms at the metric).
 #ifndef ACMMP_INIT_VB
-#define ACMMP_INIT_VB 2
+#define ACMMP_INIT_VB 4
 #endif
 [[maybe_unused]] constexpr int kInitVB = ACMMP_INIT_VB;
 
