@@ -1589,7 +1589,10 @@ __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour
 #define ACMMP_NB_WAVES_FM 7                 // the fast-math instances: 72 VGPRs, no spills (r02 A/B: 7 waves +0.6% over 8)
 #endif
 template <int MODEL, int VB, int TEX, int FM>
-__global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_WAVES_FM : ACMMP_NB_WAVES) : 1) void k_eval_nb(
+#ifndef ACMMP_NB_WAVES_PIN
+#define ACMMP_NB_WAVES_PIN 1                // pinhole instances: no register budget
+#endif
+__global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_WAVES_FM : ACMMP_NB_WAVES) : ACMMP_NB_WAVES_PIN) void k_eval_nb(
     const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
