@@ -74,7 +74,9 @@ def parse():
                     help="engine arithmetic (acmmp_set_math): fast = the reference's --use_fast_math arithmetic "
                          "(tolerance parity, tests/test_gpu_fastmath.py); exact = bit-identical to the oracle")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other math mode beside `value`")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=25.0,
+                    help="target length of the CPU-baseline sample (the probe rows sit at the equator, the "
+                         "slowest rows of the metric view: the sample takes about 55%% of this)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 -> every host core this process may use (affinity and cgroup quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
