@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <cstdlib>
 #include <vector>
 
 #include "acmmp.h"
@@ -28,17 +29,32 @@ constexpr double kMPi = 3.14159265358979323846;  // M_PI
 
 struct Pt { long long x, y; };
 
-inline long long orient(const Pt& a, const Pt& b, const Pt& c) {
-    return (b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x);
-}
-
-// > 0 when d lies strictly inside the circumcircle of the counter-clockwise triangle (a, b, c)
-inline int incircle(const Pt& a, const Pt& b, const Pt& c, const Pt& d) {
+inline int incircle128(const Pt& a, const Pt& b, const Pt& c, const Pt& d) {
     typedef __int128 i128;
     const i128 adx = a.x - d.x, ady = a.y - d.y, bdx = b.x - d.x, bdy = b.y - d.y, cdx = c.x - d.x, cdy = c.y - d.y;
     const i128 ad = adx * adx + ady * ady, bd = bdx * bdx + bdy * bdy, cd = cdx * cdx + cdy * cdy;
     const i128 det = ad * (bdx * cdy - bdy * cdx) - bd * (adx * cdy - ady * cdx) + cd * (adx * bdy - ady * bdx);
     return det > 0 ? 1 : (det < 0 ? -1 : 0);
+}
+
+inline long long orient(const Pt& a, const Pt& b, const Pt& c) {
+    return (b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x);
+}
+
+// > 0 when d lies strictly inside the circumcircle of the counter-clockwise triangle (a, b, c).
+// Exact either way: 64-bit when every coordinate difference is below 2^14 in magnitude (terms below
+// 2^59, so the three-term sum stays below 2^63), 128-bit otherwise (the super triangle's vertices).
+inline int incircle(const Pt& a, const Pt& b, const Pt& c, const Pt& d) {
+    const long long adx = a.x - d.x, ady = a.y - d.y, bdx = b.x - d.x, bdy = b.y - d.y, cdx = c.x - d.x,
+                    cdy = c.y - d.y;
+    const long long lim = 1ll << 14;
+    if (std::llabs(adx) < lim && std::llabs(ady) < lim && std::llabs(bdx) < lim && std::llabs(bdy) < lim &&
+        std::llabs(cdx) < lim && std::llabs(cdy) < lim) {
+        const long long ad = adx * adx + ady * ady, bd = bdx * bdx + bdy * bdy, cd = cdx * cdx + cdy * cdy;
+        const long long det = ad * (bdx * cdy - bdy * cdx) - bd * (adx * cdy - ady * cdx) + cd * (adx * bdy - ady * bdx);
+        return det > 0 ? 1 : (det < 0 ? -1 : 0);
+    }
+    return incircle128(a, b, c, d);
 }
 
 struct Tri {
