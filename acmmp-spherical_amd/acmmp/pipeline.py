@@ -355,10 +355,12 @@ class Pipeline:
         self._pending = []
         self.stage_s = {}                                   # host wall seconds per stage (profiling)
         self._stage_lock = threading.Lock()
-        # planar passes: overlap a view's host planar-prior block with the next view's first
-        # RunPatchMatch (second engine context on the same GPU, one worker thread; _pass_overlapped)
-        self.overlap = overlap and gpu
-        self._engine2 = None
+        # planar passes: overlap views' host planar-prior blocks with later views' first RunPatchMatch
+        # (`overlap` engine contexts on the same GPU, as many worker threads; _pass_overlapped).
+        # overlap=True means ACMMP_PIPELINE_SLOTS (default 3) contexts; False / 1 = the sequential loop.
+        slots = int(os.environ.get("ACMMP_PIPELINE_SLOTS", "3")) if overlap is True else int(overlap or 1)
+        self.overlap = slots if (gpu and slots > 1) else 0
+        self._extra_engines = []
         self._math = math
 
     @contextlib.contextmanager
@@ -371,12 +373,16 @@ class Pipeline:
             with self._stage_lock:
                 self.stage_s[stage] = self.stage_s.get(stage, 0.0) + dt
 
+    @property
+    def _engine2(self):
+        return self._extra_engines[0] if self._extra_engines else None
+
     def close(self):
         """Release the engine context(s) this pipeline created or was given."""
-        for e in (self._engine2, self.engine):
+        for e in self._extra_engines + [self.engine]:
             if e is not None and hasattr(e, "close"):
                 e.close()
-        self._engine2 = None
+        self._extra_engines = []
 
     # -- sharding
     def owner(self, i: int) -> int:
@@ -493,19 +499,23 @@ class Pipeline:
         e.upload_views_device(bufs, cams)
 
     def _pass_overlapped(self, hier, log):
-        """A planar pass with two engine contexts on the GPU: view k's second half (host planar prior,
-        second RunPatchMatch, store) runs on a worker thread while the main thread runs view k+1's
-        first half on the other context.  The views of a planar pass are independent (each reads only
-        its own view's earlier-pass state), so the outputs are those of the sequential loop."""
-        if self._engine2 is None:
-            self._engine2 = capi.Context(self.device)
+        """A planar pass over `self.overlap` engine contexts on the GPU: view k's second half (host planar
+        prior, second RunPatchMatch, store) runs on a worker thread while the main thread runs the next
+        views' first halves on the other contexts -- several views' host planar blocks (Delaunay, on
+        the host as in the reference) in flight at once.  The views of a planar pass are independent
+        (each reads only its own view's earlier-pass state), so the outputs are those of the sequential
+        loop."""
+        n = self.overlap
+        while len(self._extra_engines) < n - 1:
+            e = capi.Context(self.device)
             if self._math is not None:
-                self._engine2.set_math(self._math)
-        engines = [self.engine, self._engine2]
-        busy = [None, None]
-        with ThreadPoolExecutor(1) as pool:
+                e.set_math(self._math)
+            self._extra_engines.append(e)
+        engines = [self.engine] + self._extra_engines[:n - 1]
+        busy = [None] * n
+        with ThreadPoolExecutor(n) as pool:
             for k, i in enumerate(self.my_problems()):
-                slot = k % 2
+                slot = k % n
                 if busy[slot] is not None:
                     busy[slot].result()                      # the context is free again
                 head = self._problem_head(i, False, True, hier, False, engines[slot])

@@ -140,16 +140,17 @@ def test_gpu_pipeline_bitexact_vs_oracle_pipeline():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("math", ["exact", "fast"])
-def test_gpu_pipeline_overlapped_planar_passes_equal_sequential(math):
-    """Planar passes on two engine contexts with a view's planar block overlapping the next view's first
-    RunPatchMatch (Pipeline(overlap=True), the default) store exactly what the sequential loop stores."""
-    ds = small_dataset(64, 32, 4)
-    a = pipeline.Pipeline(ds, order="reference", size_bound=40, math=math).run()
+@pytest.mark.parametrize("math,slots", [("exact", True), ("fast", True), ("exact", 2), ("fast", 4)])
+def test_gpu_pipeline_overlapped_planar_passes_equal_sequential(math, slots):
+    """Planar passes on several engine contexts, views' planar blocks overlapping later views' first
+    RunPatchMatch (Pipeline(overlap=True), the default: 3 contexts) store exactly what the sequential
+    loop stores."""
+    ds = small_dataset(64, 32, 5)
+    a = pipeline.Pipeline(ds, order="reference", size_bound=40, math=math, overlap=slots).run()
     b = pipeline.Pipeline(ds, order="reference", size_bound=40, math=math, overlap=False).run()
     assert a._engine2 is not None and b._engine2 is None
     ma, mb = final_maps(a), final_maps(b)
-    assert ma.keys() == mb.keys() and len(ma) >= 16
+    assert ma.keys() == mb.keys() and len(ma) >= 20
     for k in mb:
         assert_bitwise_equal(ma[k], mb[k], str(k))
     a.close()
