@@ -28,34 +28,39 @@ constexpr int kSphere = 11;
 constexpr int kMaxViews = 32;       // cost_vector[32], uint32 view bitmask (ACMMP.cu:522,1153)
 
 struct DevCam {
+    // The fields the fast-math sample loop reads come first, contiguous and 16-byte aligned, so each
+    // view's constants arrive in a few wide scalar loads (s_load_dwordx16 + x4 + x2 per sample and
+    // view instead of nine narrow ones; r02 A/B profiles/r02_cam_layout_ab.txt: k_eval_nb -1.3%).
+    // The fast projection works in the reference camera's frame: a source point is FR q + Ft for the
+    // camera-frame point q = depth * ray of the reference pixel, FR = K R R0^T and Ft = K (R C0 + t)
+    // (K = identity for SPHERE; R0, C0: the problem's reference camera, rounded once from doubles).
+    float FR[9], Ft[3];
+    float fkx, fky;                 // SPHERE: W / (2 pi), H / pi (fast mode)
+    float cx, cy;                   // SPHERE params[1], params[2]
+    // binary16 copy of the padded image (same layout, 2 B per texel), present when every texel of
+    // every view is exactly representable (8-bit images are): half the cache footprint, same values
+    const uint16_t* img16_base;
+    int img16_bytes;
+    float invW;                     // 1/W             (SPHERE longitude wrap)
+    float Wf;
+    float Hm1f;                     // H - 1 as float (SPHERE row clamp)
+    int Wm1;                        // W - 1 (texel clamp)
+    int pitch4;                     // bytes per padded row
+    // the rest
     int model, W, H, img_pitch;     // img_pitch: floats per padded row (W + 2)
     float R[9];
     float t[3];
     float K[9];
-    float cx, cy;                   // SPHERE params[1], params[2]
     float inv_fx, inv_fy;           // 1/K[0], 1/K[4]  (pinhole world point)
-    float invW;                     // 1/W             (SPHERE longitude wrap)
-    float Wf, Hf;
+    float Hf;
     float C[3];                     // camera centre -(R^T t), computed like ACMMP.cu:592-594
     long long img_off;              // float offset of padded texel (-1,-1)
     long long dep_off;              // float offset of the geom depth map (row-major)
     int dep_w, dep_h;
     int img_bytes;                  // bytes of the padded image (buffer descriptor range)
-    int Wm1, Hm1;                   // W - 1, H - 1 (texel clamps)
-    float Hm1f;                     // H - 1 as float (SPHERE row clamp)
-    int pitch4;                     // bytes per padded row
+    int Hm1;                        // H - 1 (texel clamp)
     const float* img_base;          // device address of padded texel (-1,-1) (buffer descriptor base)
-    // binary16 copy of the padded image (same layout, 2 B per texel), present when every texel of
-    // every view is exactly representable (8-bit images are): half the cache footprint, same values
-    const uint16_t* img16_base;
-    int img16_bytes;
     int pitch2;                     // bytes per padded binary16 row
-    // fast-math projection constants (KParams::fast)
-    float fkx, fky;                 // SPHERE: W / (2 pi), H / pi
-    // the fast projection in the reference camera's frame: a source point is FR q + Ft for the
-    // camera-frame point q = depth * ray of the reference pixel, FR = K R R0^T and Ft = K (R C0 + t)
-    // (K = identity for SPHERE; R0, C0: the problem's reference camera, rounded once from doubles)
-    float FR[9], Ft[3];
 };
 
 // Per-pixel state handed from k_select to k_eval_ref / k_finish (80 bytes).
