@@ -1012,9 +1012,13 @@ static int run_rows(const or_problem *pb, const or_params *pp, or_state *st, uin
 
     if (row0 < 0) row0 = 0;
     if (row1 > H) row1 = H;
-#pragma omp parallel for schedule(dynamic, 4)
-    for (int y = row0; y < row1; ++y)
-        for (int x = 0; x < W; ++x) init_pixel(&cx, st, x, y, &rng[(size_t)y * W + x]);
+    /* pixels are independent within a step: parallel over pixels, not rows, so a few-row band
+       (the bench's CPU sample) still spreads over every thread */
+#pragma omp parallel for schedule(dynamic, 256)
+    for (long i = (long)row0 * W; i < (long)row1 * W; ++i) {
+        const int y = (int)(i / W), x = (int)(i % W);
+        init_pixel(&cx, st, x, y, &rng[(size_t)i]);
+    }
 
     if (n_half_sweeps < 0) n_half_sweeps = 2 * pp->max_iterations;
     const int rows = checker_rows(H) < row1 ? checker_rows(H) : row1;
@@ -1024,10 +1028,12 @@ static int run_rows(const or_problem *pb, const or_params *pp, or_state *st, uin
         memcpy(costs2, st->costs, sizeof(float) * P);
         memcpy(sel2, st->selected_views, sizeof(uint32_t) * P);
         or_state in = { planes2, costs2, st->pre_costs, sel2 };
-#pragma omp parallel for schedule(dynamic, 2)
-        for (int y = row0; y < rows; ++y)
-            for (int x = (y + colour) & 1; x < W; x += 2)
-                propagate_pixel(&cx, &in, st, &rng[(size_t)y * W + x], x, y, iter);
+        const int Wh = (W + 1) / 2;     /* pixels of this colour per row, at most */
+#pragma omp parallel for schedule(dynamic, 64)
+        for (long i = (long)row0 * Wh; i < (long)rows * Wh; ++i) {
+            const int y = (int)(i / Wh), x = (int)(i % Wh) * 2 + ((y + colour) & 1);
+            if (x < W) propagate_pixel(&cx, &in, st, &rng[(size_t)y * W + x], x, y, iter);
+        }
     }
 
     if (do_post) {
