@@ -261,7 +261,9 @@ __device__ __forceinline__ float depth_from_plane(float4 ph, float4 d) {
 #define ACMMP_FM_GUARD 0                    // fast mode: the |t| < 1e-6 test costs 3 VALU per view-sample
 #endif                                      // (r02 A/B profiles/r02_micro_ab.txt: metric +2%, C3 +1.8%)
 // Chunks whose VB views are all present compile without per-view guards (one basic block per sample):
-// pinhole +17% at C2 (V = 10: its 8-view chunk), SPHERE -1..-2% (longer live ranges), so pinhole only
+// pinhole +17% at C2 (V = 10: its 8-view chunk).  SPHERE (ACMMP_FULL_CHUNK_SPH: 0 never, 1 always,
+// 2 = chunks of at most 2 views outside k_eval_nb): k_eval_nb's 4-view chunks -1..-3% (longer live
+// ranges), k_eval_ref's 2-view chunks at V = 15 +4.7% (r02 A/B profiles/r02_full_chunk_ab.txt)
 #ifndef ACMMP_FULL_CHUNK_PIN
 #define ACMMP_FULL_CHUNK_PIN 1
 #endif
@@ -269,7 +271,7 @@ __device__ __forceinline__ float depth_from_plane(float4 ph, float4 d) {
 #define ACMMP_VIEW_BARRIER 1
 #endif
 #ifndef ACMMP_FULL_CHUNK_SPH
-#define ACMMP_FULL_CHUNK_SPH 0
+#define ACMMP_FULL_CHUNK_SPH 2
 #endif
 
 // atan(t) on [0, 1]: t + t^3 P(t^2), 7-term minimax, max |error| 1.1e-7 rad
@@ -910,7 +912,9 @@ __device__ __forceinline__ void for_all_views_t(const KParams& kp, int px, int p
         }
         if (nv == 0) break;
         float cost[VB];
-        if ((MODEL == kSphere ? ACMMP_FULL_CHUNK_SPH : ACMMP_FULL_CHUNK_PIN) && VB > 1 && nv == VB)
+        constexpr bool kFullSph = ACMMP_FULL_CHUNK_SPH == 1 || (ACMMP_FULL_CHUNK_SPH == 2 && VB <= 2) ||
+                                  (ACMMP_FULL_CHUNK_SPH == 3 && VB <= 2 && STAGED == 3);
+        if ((MODEL == kSphere ? kFullSph : ACMMP_FULL_CHUNK_PIN) && VB > 1 && nv == VB)
             ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM, true>(kp, px, py, pt, ph, vlist, nv, cost);
         else
             ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM>(kp, px, py, pt, ph, vlist, nv, cost);
