@@ -653,6 +653,24 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
 #define ACMMP_NV_UNIFORM 1
 #endif
     const int nv = FULL ? VB : (ACMMP_NV_UNIFORM ? uniform_int(nv_rt) : nv_rt);
+    // per-view guard inside the sample loop: `v < nv` hoisted out of the loop is an i1 live across it,
+    // which the backend keeps as a lane mask and re-tests through a VGPR (v_cndmask + v_cmp per
+    // view-sample); re-reading nv into an SGPR at the use keeps the test a scalar compare.  Applied to
+    // SPHERE k_eval_nb-layout chunks (ACMMP_NV_SCALAR_GUARD 2): k_eval_nb -1.5..-2% there, while the
+    // pinhole refinement (+2.7%) and k_select (+3%) lose (r02 A/B profiles/r02_nv_guard_ab.txt)
+#ifndef ACMMP_NV_SCALAR_GUARD
+#define ACMMP_NV_SCALAR_GUARD 2
+#endif
+    constexpr bool kScalarGuard = ACMMP_NV_SCALAR_GUARD == 1 || (ACMMP_NV_SCALAR_GUARD == 2 && MODEL == kSphere && STAGED == 3);
+    auto has = [&](int v) -> bool {
+        if (FULL) return true;
+        if constexpr (kScalarGuard) {
+            int n;
+            asm volatile("s_mov_b32 %0, %1" : "=s"(n) : "s"(nv));
+            return v < n;
+        }
+        return v < nv;
+    };
     // SPHERE: the weight sum of every view is the pixel's patch sum (hypothesis- and view-independent);
     // below 1e-6 each cost is 2.0 (ACMMP.cu:501-503) whatever the samples, so they are not evaluated.
     // (The SPHERE sigma-in-radians band of SURVEY.md §0.5 puts ~40% of a 2000x1500 view here.)
@@ -739,7 +757,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
 #define ACMMP_ACCUMULATE(v)                                                  \
             do {                                                             \
                 const float sp = lerp_tap<TEX>(tap[v]);                      \
-                if (MODEL == kSphere ? (v < nv) : ok[v]) {                   \
+                if (MODEL == kSphere ? has(v) : ok[v]) {                     \
                     if (MODEL == kPinhole) {                                 \
                         sbw[v] += w;                                         \
                         sref[v] = fmaf(w, r, sref[v]);                       \
@@ -754,7 +772,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
                 ok[v] = false;
-                if (v < nv) {
+                if (has(v)) {
                     ConstCam& c = PCV(v);
                     float sx, sy, sd;
                     if (FM) project_fast<MODEL>(c, P, sx, sy);
@@ -780,7 +798,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 if (G > 1 && ((v + 1) % G == 0 || v == VB - 1)) {
 #pragma unroll
                     for (int u = v - (v % G); u <= v; ++u)
-                        if (u < nv) ACMMP_ACCUMULATE(u);
+                        if (has(u)) ACMMP_ACCUMULATE(u);
                 }
             }
 #undef ACMMP_ACCUMULATE
