@@ -656,12 +656,13 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     // per-view guard inside the sample loop: `v < nv` hoisted out of the loop is an i1 live across it,
     // which the backend keeps as a lane mask and re-tests through a VGPR (v_cndmask + v_cmp per
     // view-sample); re-reading nv into an SGPR at the use keeps the test a scalar compare.  Applied to
-    // SPHERE k_eval_nb-layout chunks (ACMMP_NV_SCALAR_GUARD 2): k_eval_nb -1.5..-2% there, while the
-    // pinhole refinement (+2.7%) and k_select (+3%) lose (r02 A/B profiles/r02_nv_guard_ab.txt)
+    // fast-mode SPHERE k_eval_nb-layout chunks (ACMMP_NV_SCALAR_GUARD 2): k_eval_nb -1.5..-2% there,
+    // while the pinhole refinement (+2.7%), k_select (+3%) and the exact-mode k_eval_nb (+0.7%) lose
+    // (r02 A/B profiles/r02_nv_guard_ab.txt)
 #ifndef ACMMP_NV_SCALAR_GUARD
 #define ACMMP_NV_SCALAR_GUARD 2
 #endif
-    constexpr bool kScalarGuard = ACMMP_NV_SCALAR_GUARD == 1 || (ACMMP_NV_SCALAR_GUARD == 2 && MODEL == kSphere && STAGED == 3);
+    constexpr bool kScalarGuard = ACMMP_NV_SCALAR_GUARD == 1 || (ACMMP_NV_SCALAR_GUARD == 2 && MODEL == kSphere && STAGED == 3 && FM);
     auto has = [&](int v) -> bool {
         if (FULL) return true;
         if constexpr (kScalarGuard) {
