@@ -754,11 +754,17 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             const float wr = w * r;
             Tap tap[VB];
             bool ok[VB];
+            // ACMMP_ACC_ALL: with scalar guards, accumulate every view of the chunk without a guard (views
+            // past nv accumulate view 0's texel into sums nobody reads), so the accumulation is one block
+#ifndef ACMMP_ACC_ALL
+#define ACMMP_ACC_ALL 0                     // 1: k_eval_nb +3.5..4.5% (profiles/r02_acc_all_ab.txt)
+#endif
+            constexpr bool kAccAll = ACMMP_ACC_ALL && kScalarGuard && G > 1;
             // accumulate view v's sample (ACMMP.cu:488-498)
 #define ACMMP_ACCUMULATE(v)                                                  \
             do {                                                             \
                 const float sp = lerp_tap<TEX>(tap[v]);                      \
-                if (MODEL == kSphere ? has(v) : ok[v]) {                     \
+                if (MODEL == kSphere ? (kAccAll || has(v)) : ok[v]) {       \
                     if (MODEL == kPinhole) {                                 \
                         sbw[v] += w;                                         \
                         sref[v] = fmaf(w, r, sref[v]);                       \
@@ -790,6 +796,8 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(c.img_base), 0, c.img_bytes, 0x00020000);
                     tap[v] = fetch_tap<TEX, MODEL == kSphere>(rs, c, sx, sy);
                     if (G == 1) ACMMP_ACCUMULATE(v);
+                } else if (kAccAll) {
+                    tap[v] = tap[0];
                 }
                 // a full SPHERE chunk has no per-view branches; keep its views' code in view order
                 // (interleaved, their live ranges overlap and the 7-wave register budget spills)
@@ -799,7 +807,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 if (G > 1 && ((v + 1) % G == 0 || v == VB - 1)) {
 #pragma unroll
                     for (int u = v - (v % G); u <= v; ++u)
-                        if (has(u)) ACMMP_ACCUMULATE(u);
+                        if (kAccAll || has(u)) ACMMP_ACCUMULATE(u);
                 }
             }
 #undef ACMMP_ACCUMULATE
