@@ -289,12 +289,15 @@ __device__ __forceinline__ float atan_core_fast(float t) {
 
 // P: the sample's point in the REFERENCE camera's frame (depth * ray); FR / Ft map it into the source
 // camera (DevCam::FR, set per problem), so no world point is formed per sample.
+// ft: the translation Ft, from the camera (nullptr) or from registers the caller holds (a VOP3 fma reads
+// one SGPR, so a translation in SGPRs costs a move per row and view-sample)
 template <int MODEL, typename Cam>
-__device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float& oy) {
+__device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float& oy, const float* ft = nullptr) {
     if (MODEL == kSphere) {
-        const float tx = fmaf(c.FR[2], P.z, fmaf(c.FR[1], P.y, fmaf(c.FR[0], P.x, c.Ft[0])));
-        const float ty = fmaf(c.FR[5], P.z, fmaf(c.FR[4], P.y, fmaf(c.FR[3], P.x, c.Ft[1])));
-        const float tz = fmaf(c.FR[8], P.z, fmaf(c.FR[7], P.y, fmaf(c.FR[6], P.x, c.Ft[2])));
+        const float f0 = ft ? ft[0] : c.Ft[0], f1 = ft ? ft[1] : c.Ft[1], f2 = ft ? ft[2] : c.Ft[2];
+        const float tx = fmaf(c.FR[2], P.z, fmaf(c.FR[1], P.y, fmaf(c.FR[0], P.x, f0)));
+        const float ty = fmaf(c.FR[5], P.z, fmaf(c.FR[4], P.y, fmaf(c.FR[3], P.x, f1)));
+        const float tz = fmaf(c.FR[8], P.z, fmaf(c.FR[7], P.y, fmaf(c.FR[6], P.x, f2)));
         const float r2 = fmaf(tz, tz, fmaf(ty, ty, tx * tx));
         // -latitude = asin(ty / |t|) (ProjectonCamera_cu :626-630)
         const float s = __builtin_amdgcn_fmed3f(ty * __builtin_amdgcn_rsqf(r2), -1.0f, 1.0f);
@@ -706,6 +709,19 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             cval[v] = !(ox < 0.0f || ox >= PCV(v).Wf || oy < 0.0f || oy >= PCV(v).Hf);
         }
     }
+    // ACMMP_FT_VGPR: fast-mode SPHERE k_eval_nb chunks hold each view's Ft in VGPRs across the loop
+#ifndef ACMMP_FT_VGPR
+#define ACMMP_FT_VGPR 1                     // k_eval_nb -1.3..-1.7%, metric +1% (profiles/r02_ft_vgpr_ab.txt)
+#endif
+    constexpr bool kFtV = ACMMP_FT_VGPR && FM && MODEL == kSphere && STAGED == 3;
+    float ftv[VB][3];
+#pragma unroll
+    for (int v = 0; v < VB; ++v)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            ftv[v][k] = 0.f;
+            if (kFtV) asm volatile("v_mov_b32 %0, %1" : "=v"(ftv[v][k]) : "s"(PCV(v).Ft[k]));
+        }
     const int R = kp.R, inc = kp.inc;
     constexpr int G = PIPE ? VB : (TEX == 1 ? kPipeG16 : kPipeG);
     int s = 0, ii = 0;
@@ -782,7 +798,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 if (has(v)) {
                     ConstCam& c = PCV(v);
                     float sx, sy, sd;
-                    if (FM) project_fast<MODEL>(c, P, sx, sy);
+                    if (FM) project_fast<MODEL>(c, P, sx, sy, kFtV ? ftv[v] : nullptr);
                     else project<MODEL>(c, P, sx, sy, sd);
                     ok[v] = true;
                     if (MODEL == kSphere) {
