@@ -292,7 +292,8 @@ __device__ __forceinline__ float atan_core_fast(float t) {
 // ft: the translation Ft, from the camera (nullptr) or from registers the caller holds (a VOP3 fma reads
 // one SGPR, so a translation in SGPRs costs a move per row and view-sample)
 template <int MODEL, typename Cam>
-__device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float& oy, const float* ft = nullptr) {
+__device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float& oy, const float* ft = nullptr,
+                                             const float* cc = nullptr) {
     if (MODEL == kSphere) {
         const float f0 = ft ? ft[0] : c.Ft[0], f1 = ft ? ft[1] : c.Ft[1], f2 = ft ? ft[2] : c.Ft[2];
         const float tx = fmaf(c.FR[2], P.z, fmaf(c.FR[1], P.y, fmaf(c.FR[0], P.x, f0)));
@@ -312,8 +313,8 @@ __device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float&
         r = ay > ax ? kPio2Hi - r : r;
         r = __builtin_bit_cast(int, tz) < 0 ? kPiHi - r : r;
         const float lon = copysignf(r, tx);
-        ox = fmaf(lon, c.fkx, c.cx);
-        oy = fmaf(neg_lat, c.fky, c.cy);
+        ox = fmaf(lon, c.fkx, cc ? cc[0] : c.cx);
+        oy = fmaf(neg_lat, c.fky, cc ? cc[1] : c.cy);
         // |t| < 1e-6 (:618-622): a sample on a source camera's centre.  ACMMP_FM_GUARD 0 drops the
         // test: such a sample then projects to NaN and its view's cost is 2.0 (the NCC clamp) -- the
         // reference's tex2D of (cx, cy) there is as meaningless, and no real geometry reaches it
@@ -714,14 +715,24 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
 #define ACMMP_FT_VGPR 1                     // k_eval_nb -1.3..-1.7%, metric +1% (profiles/r02_ft_vgpr_ab.txt)
 #endif
     constexpr bool kFtV = ACMMP_FT_VGPR && FM && MODEL == kSphere && STAGED == 3;
-    float ftv[VB][3];
+#ifndef ACMMP_CC_VGPR
+#define ACMMP_CC_VGPR 0                     // the same for (cx, cy): 74 VGPRs / 6 waves, not yet measured
+#endif
+    constexpr bool kCcV = kFtV && ACMMP_CC_VGPR;
+    float ftv[VB][3], ccv[VB][2];
 #pragma unroll
-    for (int v = 0; v < VB; ++v)
+    for (int v = 0; v < VB; ++v) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             ftv[v][k] = 0.f;
             if (kFtV) asm volatile("v_mov_b32 %0, %1" : "=v"(ftv[v][k]) : "s"(PCV(v).Ft[k]));
         }
+        ccv[v][0] = ccv[v][1] = 0.f;
+        if (kCcV) {
+            asm volatile("v_mov_b32 %0, %1" : "=v"(ccv[v][0]) : "s"(PCV(v).cx));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(ccv[v][1]) : "s"(PCV(v).cy));
+        }
+    }
     const int R = kp.R, inc = kp.inc;
     constexpr int G = PIPE ? VB : (TEX == 1 ? kPipeG16 : kPipeG);
     int s = 0, ii = 0;
@@ -798,7 +809,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 if (has(v)) {
                     ConstCam& c = PCV(v);
                     float sx, sy, sd;
-                    if (FM) project_fast<MODEL>(c, P, sx, sy, kFtV ? ftv[v] : nullptr);
+                    if (FM) project_fast<MODEL>(c, P, sx, sy, kFtV ? ftv[v] : nullptr, kCcV ? ccv[v] : nullptr);
                     else project<MODEL>(c, P, sx, sy, sd);
                     ok[v] = true;
                     if (MODEL == kSphere) {
