@@ -200,9 +200,11 @@ class Context:
                 raise ValueError(f"image {i} has shape {tuple(shp)}, camera says {int(cam['height'])}x{int(cam['width'])}")
 
     def _check_hw(self, arr, tail, what):
+        """Row-major (H, W)+tail maps, or the same elements flat: any other shape (a transposed
+        (W, H) map with the right element count included) is refused, not read in the wrong layout."""
         want = (self.H, self.W) + tail
-        if arr.shape != want and arr.size != int(np.prod(want)):
-            raise ValueError(f"{what}: shape {arr.shape}, expected {want}")
+        if arr.shape != want and arr.shape != (int(np.prod(want)),):
+            raise ValueError(f"{what}: shape {arr.shape}, expected {want} (or flat {int(np.prod(want))})")
 
     def upload_views(self, images, cameras):
         imgs = [np.ascontiguousarray(im, np.float32) for im in images]

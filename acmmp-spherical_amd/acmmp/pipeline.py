@@ -362,6 +362,8 @@ class Pipeline:
         self.overlap = slots if (gpu and slots > 1) else 0
         self._extra_engines = []
         self._math = math
+        if gpu:
+            self.log(f"engine math: {self.engine.math()}")
 
     @contextlib.contextmanager
     def _timed(self, stage):
@@ -752,7 +754,7 @@ def main(argv=None):
     ap.add_argument("--geom-iterations", type=int, default=2)
     ap.add_argument("--size-bound", type=int, default=1000, help="coarsest-scale bound (main.cpp:38)")
     ap.add_argument("--math", choices=["exact", "fast"], default=None,
-                    help="engine arithmetic (default: exact, or ACMMP_MATH from the environment)")
+                    help="engine arithmetic (default: exact, bit-identical to the oracle)")
     ap.add_argument("--no-dmb", action="store_true", help="keep results in memory only")
     ap.add_argument("--no-fusion", action="store_true", help="skip RunFusionCuda")
     a = ap.parse_args(argv)

@@ -225,7 +225,7 @@ acmmp_status acmmp_create(int device, acmmp_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return ACMMP_ERR_HIP;
     acmmp_ctx* c = new acmmp_ctx();
     c->device = device;
-    if (const char* m = std::getenv("ACMMP_MATH")) c->math = (m[0] == 'f') ? ACMMP_MATH_FAST : ACMMP_MATH_EXACT;
+    // math stays ACMMP_MATH_EXACT (bit-identical to the oracle) until the caller picks fast explicitly
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return ACMMP_ERR_HIP;

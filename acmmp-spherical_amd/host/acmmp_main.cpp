@@ -39,7 +39,7 @@ struct Options {
     std::string dense_folder;
     uint64_t seed = 1234;
     int device = 0;
-    int math = -1;              // -1: the engine's default (ACMMP_MATH or exact)
+    int math = -1;              // -1: the engine's default (exact); --math fast to opt in
     bool fusion = true;
     int geom_iterations = 2;
     int size_bound = 1000;      // main.cpp:38 (the coarsest scale's bound); tests use small scenes
@@ -278,6 +278,11 @@ int main(int argc, char** argv) {
     if (opt.math >= 0 && acmmp_set_math(ctx, opt.math) != ACMMP_OK) {
         std::printf("acmmp_set_math failed\n");
         return EXIT_FAILURE;
+    }
+    {
+        const int m = acmmp_get_math(ctx);
+        std::cout << "Engine math: " << (m == ACMMP_MATH_FAST ? "fast (--use_fast_math arithmetic, tolerance parity)"
+                                                               : "exact (bit-identical to the CPU oracle)") << std::endl;
     }
 
     int flag = 0, pass = 0;

@@ -1,6 +1,10 @@
 // jpeg.cpp -- see jpeg.hpp.  Restated from the JPEG standard (ITU T.81) and the published
-// algorithms of libjpeg-turbo's decoder (jidctint.c, jdsample.c, jdcolor.c, jdmainct.c); written
-// for this driver, no source shared with either.
+// algorithms of libjpeg-turbo's decoder (jidctint.c, jdsample.c, jdcolor.c, jdmainct.c), written for
+// this driver so that it decodes bit-identically to the library OpenCV's imread uses.  Credit: the
+// integer IDCT `idct_islow` follows the Independent JPEG Group's jpeg_idct_islow (jidctint.c, as kept
+// in libjpeg-turbo) step for step -- its LL&M factorisation, CONST_BITS/PASS1_BITS scaling, the
+// tmp0..3 / z1..z5 intermediates and the zero-AC column shortcut -- because bit parity with that
+// library requires the same rounding points (IJG licence: this notice acknowledges the IJG's work).
 #include "jpeg.hpp"
 
 #include <algorithm>
@@ -103,6 +107,7 @@ private:
                     if (!dqt(seg, end, err)) return false;
                     break;
                 case 0xDD:
+                    if (end - seg < 2) return fail(err, "bad DRI");
                     restart_ = (d_[seg] << 8) | d_[seg + 1];
                     break;
                 case 0xE0:
@@ -146,6 +151,8 @@ private:
             hmax_ = std::max(hmax_, c.h);
             vmax_ = std::max(vmax_, c.v);
         }
+        for (int i = 0; i < ncomp_; ++i)       // upsample() needs integral ratios (libjpeg rejects the rest)
+            if (hmax_ % comp_[i].h || vmax_ % comp_[i].v) return fail(err, "unsupported sampling factors");
         mcux_ = (W_ + 8 * hmax_ - 1) / (8 * hmax_);
         mcuy_ = (H_ + 8 * vmax_ - 1) / (8 * vmax_);
         for (int i = 0; i < ncomp_; ++i) {
@@ -164,6 +171,7 @@ private:
         while (p < end) {
             const int pq = d_[p] >> 4, tq = d_[p] & 3;
             ++p;
+            if (p + (pq ? 128 : 64) > end) return fail(err, "bad DQT");
             for (int k = 0; k < 64; ++k) {
                 int v;
                 if (pq) { v = (d_[p] << 8) | d_[p + 1]; p += 2; }
@@ -171,7 +179,6 @@ private:
                 qt_[tq][kNatural[k]] = static_cast<uint16_t>(v);
             }
             qt_set_[tq] = true;
-            if (p > end) return fail(err, "bad DQT");
         }
         return true;
     }
@@ -189,11 +196,16 @@ private:
             std::memcpy(hf.vals, d_ + p, total);
             p += total;
             // canonical codes (T.81 Annex C)
-            int code = 0, k = 0;
+            int code = 0, k = 0, lastl = 0;
+            for (int l = 1; l <= 16; ++l) if (counts[l]) lastl = l;
             std::memset(hf.look, 0, sizeof hf.look);
             for (int l = 1; l <= 16; ++l) {
                 hf.valptr[l] = k;
                 hf.mincode[l] = code;
+                // every code of length l must fit in l bits and not be all ones (libjpeg's
+                // JERR_BAD_HUFF_TABLE test, applied up to the longest length in use); an
+                // oversubscribed table would index look[] past its end below
+                if (l <= lastl && code + counts[l] >= (1 << l)) return fail(err, "bad DHT");
                 for (int i = 0; i < counts[l]; ++i, ++k, ++code)
                     if (l <= 8)
                         for (int fill = 0; fill < (1 << (8 - l)); ++fill)

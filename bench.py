@@ -84,7 +84,14 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true", help="skip the end-to-end ProcessProblem schedule timing")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_propagate.json"),
                     help="rocprofv3 PMC summary giving HBM bytes per propagation launch")
+    ap.add_argument("--allow-shared-gpus", action="store_true",
+                    help="rehearsal only: let more ranks than GPUs share devices round-robin (never a scaling point)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch/rendezvous check: ranks join the gloo group, agree on the world and exit without "
+                         "touching a GPU (the CPU test of `--gpus N`)")
     a = ap.parse_args()
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
     pipe = a.mode == "pipeline"        # BASELINE.json configs[3] shape vs the headline metric's
     for k, head, pl in (("width", 2000, 3200), ("height", 1500, 2133), ("n_src", 4, 20), ("model", "sphere", "pinhole")):
         if getattr(a, k) is None:
@@ -369,17 +376,81 @@ def pipeline_mode(args, rank, world, local_rank, barrier, allmax):
     return line
 
 
-def main():
-    args = parse()
-    if args.mode == "pipeline":
-        return main_pipeline(args)
+def visible_gpus() -> int:
+    """GPUs this process could use, counted without initialising a HIP runtime in it (torch's
+    device_count does not initialise the device on this image; the launcher parent never touches a
+    GPU, so it may start its children with no HIP state to inherit)."""
+    try:
+        import torch
+        return int(torch.cuda.device_count())
+    except Exception:                                                # noqa: BLE001
+        return 0
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` run directly (WORLD_SIZE unset, N > 1): start N ranks, one per GPU, as a
+    torch.distributed.run child process with the same arguments (rendezvous on 127.0.0.1, a free port),
+    wait for it and return its exit code.  Rank 0's JSON line reaches our stdout unchanged.  The parent
+    initialises nothing on a GPU and never execs."""
+    import socket
+    import subprocess
+    if not args.dry_run and not args.allow_shared_gpus:
+        ndev = visible_gpus()
+        if ndev < args.gpus:
+            print(f"bench: --gpus {args.gpus} but {ndev} GPU(s) visible; refusing to put several ranks on one "
+                  f"GPU (--allow-shared-gpus for a rehearsal)", file=sys.stderr)
+            return 2
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", str(max(1, host_cores() // args.gpus)))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dist_setup(args):
+    """(rank, world, local_rank, dist) of this process; checks the launcher agrees with --gpus."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" in os.environ and args.gpus not in (1, world):
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s)")
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         dist.init_process_group("gloo")
+    return rank, world, local_rank, dist
+
+
+def dry_run(args, rank, world, dist):
+    """--dry-run: every rank reports in over the gloo group; rank 0 prints who came."""
+    ranks = [rank]
+    if dist is not None:
+        got = [None] * world
+        dist.all_gather_object(got, {"rank": rank, "pid": os.getpid(),
+                                     "local_rank": int(os.environ.get("LOCAL_RANK", "0"))})
+        ranks = sorted(g["rank"] for g in got)
+        pids = sorted({g["pid"] for g in got})
+    else:
+        pids = [os.getpid()]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "ranks": world, "rank_ids": ranks, "processes": len(pids),
+                          "backend": dist.get_backend() if dist is not None else None, "gpus": args.gpus}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.mode == "pipeline":
+        return main_pipeline(args)
+    rank, world, local_rank, dist = dist_setup(args)
+    if args.dry_run:
+        return dry_run(args, rank, world, dist)
 
     def barrier():
         if dist is not None:
@@ -397,8 +468,11 @@ def main():
     c0 = sc.cameras[0]
     params = types.default_params(num_images=args.n_src + 1, max_iterations=args.iters,
                                   depth_min=float(c0["depth_min"]) * 0.6, depth_max=float(c0["depth_max"]) * 1.2)
-    # one GPU per rank; more ranks than GPUs (rehearsal on a small box) share them round-robin
+    # one GPU per rank; more ranks than GPUs only as an explicit rehearsal (--allow-shared-gpus)
     ndev = capi.device_count()
+    if world > max(ndev, 1) and not args.allow_shared_gpus:
+        raise SystemExit(f"bench: {world} ranks but {ndev} GPU(s) visible; one GPU per rank "
+                         f"(--allow-shared-gpus for a rehearsal)")
     ctx = capi.Context(local_rank % ndev if ndev else local_rank)
     ctx.set_math(args.math)
     ctx.set_params(params)
@@ -588,13 +662,9 @@ def main():
 
 
 def main_pipeline(args):
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # noqa: F811
-        dist.init_process_group("gloo")
+    rank, world, local_rank, dist = dist_setup(args)
+    if args.dry_run:
+        return dry_run(args, rank, world, dist)
 
     def barrier():
         if dist is not None:

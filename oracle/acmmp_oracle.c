@@ -985,11 +985,12 @@ int or_run_patchmatch(const or_problem *pb, const or_params *pp, or_state *st,
     return run_rows(pb, pp, st, seed, n_half_sweeps, do_post, nthreads, 0, pb->cams[0].height);
 }
 
-/* Bounded CPU-baseline sample: the same per-pixel work restricted to rows [row0, row1). */
+/* Bounded CPU-baseline sample and full-size parity bands: the same per-pixel work restricted to
+   rows [row0, row1); rows outside keep the state they came in with. */
 int or_run_band(const or_problem *pb, const or_params *pp, or_state *st, uint64_t seed,
-                int32_t n_half_sweeps, int32_t nthreads, int32_t row0, int32_t row1)
+                int32_t n_half_sweeps, int32_t nthreads, int32_t row0, int32_t row1, int32_t do_post)
 {
-    return run_rows(pb, pp, st, seed, n_half_sweeps, 1, nthreads, row0, row1);
+    return run_rows(pb, pp, st, seed, n_half_sweeps, do_post, nthreads, row0, row1);
 }
 
 static int run_rows(const or_problem *pb, const or_params *pp, or_state *st, uint64_t seed,

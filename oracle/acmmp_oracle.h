@@ -92,9 +92,10 @@ typedef struct or_state {
 int or_run_patchmatch(const or_problem *pb, const or_params *pp, or_state *st,
                       uint64_t seed, int32_t n_half_sweeps, int32_t do_post, int32_t nthreads);
 
-/* CPU-baseline sample: init + sweeps + post restricted to rows [row0, row1) of the same problem. */
+/* CPU-baseline sample and full-size parity bands: init + sweeps (+ post when do_post) restricted to rows
+   [row0, row1) of the same problem. */
 int or_run_band(const or_problem *pb, const or_params *pp, or_state *st, uint64_t seed,
-                int32_t n_half_sweeps, int32_t nthreads, int32_t row0, int32_t row1);
+                int32_t n_half_sweeps, int32_t nthreads, int32_t row0, int32_t row1, int32_t do_post);
 
 /* Unit entry points (T1 tests). */
 float or_bilateral_ncc(const or_problem *pb, const or_params *pp, int32_t src, int32_t px, int32_t py,

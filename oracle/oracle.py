@@ -55,7 +55,7 @@ def lib():
         vp, i32, f32 = C.c_void_p, C.c_int32, C.c_float
         L.or_run_patchmatch.argtypes = [vp, vp, vp, C.c_uint64, i32, i32, i32]
         L.or_run_patchmatch.restype = C.c_int
-        L.or_run_band.argtypes = [vp, vp, vp, C.c_uint64, i32, i32, i32, i32]
+        L.or_run_band.argtypes = [vp, vp, vp, C.c_uint64, i32, i32, i32, i32, i32]
         L.or_run_band.restype = C.c_int
         for fn in ("or_bilateral_ncc", "or_geom_cost"):
             getattr(L, fn).argtypes = [vp, vp, i32, i32, i32, vp]
@@ -162,19 +162,22 @@ def run_patchmatch_traced(prob: Problem, seed: int, **kw):
     return out
 
 
-def run_band(prob: Problem, seed: int, row0: int, row1: int, nthreads: int = 0, n_half_sweeps: int = -1):
-    """Timed CPU-baseline sample: the full per-pixel pipeline on rows [row0, row1) only."""
+def run_band(prob: Problem, seed: int, row0: int, row1: int, nthreads: int = 0, n_half_sweeps: int = -1,
+             planes=None, costs=None, pre_costs=None, selected=None, do_post: bool = True):
+    """The full per-pixel pipeline on rows [row0, row1) only (the CPU-baseline sample, and full-size
+    parity bands).  `planes` / `costs` / ... are the state a geom, planar-prior or reuse pass starts
+    from (as run_patchmatch); rows outside the band keep it untouched."""
     H, W = prob.shape
-    planes = np.zeros((H, W, 4), np.float32)
-    costs = np.zeros((H, W), np.float32)
-    pre = np.zeros((H, W), np.float32)
-    sel = np.zeros((H, W), np.uint32)
+    planes = np.zeros((H, W, 4), np.float32) if planes is None else np.array(planes, np.float32, copy=True)
+    costs = np.zeros((H, W), np.float32) if costs is None else np.array(costs, np.float32, copy=True)
+    pre = np.zeros((H, W), np.float32) if pre_costs is None else np.array(pre_costs, np.float32, copy=True)
+    sel = np.zeros((H, W), np.uint32) if selected is None else np.array(selected, np.uint32, copy=True)
     st = _State(planes.ctypes.data, costs.ctypes.data, pre.ctypes.data, sel.ctypes.data)
     rc = lib().or_run_band(C.byref(prob.struct), prob.params.ctypes.data, C.byref(st), C.c_uint64(seed),
-                           n_half_sweeps, nthreads, row0, row1)
+                           n_half_sweeps, nthreads, row0, row1, int(do_post))
     if rc != 0:
         raise RuntimeError(f"or_run_band failed ({rc})")
-    return {"planes": planes, "costs": costs}
+    return {"planes": planes, "costs": costs, "pre_costs": pre, "selected_views": sel}
 
 
 def ncc(prob: Problem, src: int, px: int, py: int, plane) -> float:

@@ -104,6 +104,51 @@ def test_jpeg_decoder_refuses_progressive_and_garbage(host, tmp_path):
         decode(lib, tmp_path / "missing.jpg", 0)
 
 
+def test_jpeg_decoder_rejects_malformed_tables(host, tmp_path):
+    """Malformed segments fail with an error instead of writing past the decoder's tables (libjpeg's
+    JERR_BAD_HUFF_TABLE / truncated DQT / short DRI / non-integral sampling ratios)."""
+    from PIL import Image
+    lib, _ = host
+    p = tmp_path / "ok.jpg"
+    Image.fromarray(synthetic_rgb(np.random.default_rng(1), 48, 32), "RGB").save(p, subsampling=2, quality=80)
+    good = p.read_bytes()
+    assert decode(lib, p, 1).shape == (32, 48, 3)
+
+    def with_segment(marker, payload):
+        seg = bytes([0xFF, marker]) + (len(payload) + 2).to_bytes(2, "big") + payload
+        return good[:2] + seg + good[2:]
+
+    cases = {
+        # DC table 0 with three 1-bit codes (only two exist): oversubscribed
+        "dht_over": with_segment(0xC4, bytes([0x00, 3] + [0] * 15) + bytes([0, 1, 2])),
+        # 255 one-bit codes
+        "dht_255": with_segment(0xC4, bytes([0x10, 255] + [0] * 15) + bytes(range(255))),
+        # a complete length-1 table uses the all-ones code, which T.81 forbids
+        "dht_all_ones": with_segment(0xC4, bytes([0x00, 2] + [0] * 15) + bytes([0, 1])),
+        "dqt_truncated": with_segment(0xDB, bytes([0x00]) + bytes(10)),
+        "dqt16_truncated": with_segment(0xDB, bytes([0x10]) + bytes(64)),
+        "dri_short": with_segment(0xDD, b""),
+    }
+    sof = good.index(b"\xff\xc0")
+    bad_sf = bytearray(good)
+    assert bad_sf[sof + 9] == 3                                  # three components
+    bad_sf[sof + 11] = 0x32                                      # Y: h=3 v=2 with Cb/Cr h=1 ok, so
+    bad_sf[sof + 14] = 0x21                                      # Cb: h=2 -> hmax 3 % 2 != 0
+    cases["sampling"] = bytes(bad_sf)
+    expect = {"dht_over": "bad DHT", "dht_255": "bad DHT", "dht_all_ones": "bad DHT", "dqt_truncated": "bad DQT",
+              "dqt16_truncated": "bad DQT", "dri_short": "bad DRI", "sampling": "unsupported sampling factors"}
+    for name, data in cases.items():
+        q = tmp_path / f"{name}.jpg"
+        q.write_bytes(data)
+        with pytest.raises(ValueError, match=expect[name]):
+            decode(lib, q, 1)
+    # a valid table (codes 0, 10, 110) is still accepted by the parser
+    ok = with_segment(0xC4, bytes([0x01, 1, 1, 1] + [0] * 13) + bytes([0, 1, 2]))
+    q = tmp_path / "dht_ok.jpg"
+    q.write_bytes(ok)
+    assert decode(lib, q, 1).shape == (32, 48, 3)
+
+
 def test_resize_and_dims_equal_python_restatement(host):
     lib, _ = host
     rng = np.random.default_rng(7)
