@@ -36,7 +36,8 @@ EXPORTS = [
     "acmmp_band_begin", "acmmp_band_sweep", "acmmp_band_sweeps_left", "acmmp_band_halo_ranges",
     "acmmp_band_copy_rows", "acmmp_band_end",
     "acmmp_fusion_create", "acmmp_fusion_set_view", "acmmp_fusion_run", "acmmp_fusion_last_error",
-    "acmmp_fusion_destroy",
+    "acmmp_fusion_destroy", "acmmp_image_cache_create", "acmmp_image_cache_destroy", "acmmp_image_cache_stats",
+    "acmmp_upload_views_keyed",
 ]
 
 
@@ -118,14 +119,19 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_planar_prior_host.argtypes = [vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]
     L.acmmp_set_planar_prior_from_maps.argtypes = [vp, vp, vp, C.c_float, C.c_float, vp]
     L.acmmp_download_planar_prior.argtypes = [vp, vp, vp]
+    L.acmmp_image_cache_create.argtypes = [i32, C.c_size_t, C.POINTER(vp)]
+    L.acmmp_image_cache_destroy.argtypes = [vp]
+    L.acmmp_image_cache_stats.argtypes = [vp, vp]
+    L.acmmp_upload_views_keyed.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32]
     for name in EXPORTS:
         fn = getattr(L, name)
         if name not in ("acmmp_destroy", "acmmp_status_str", "acmmp_last_error", "acmmp_abi_version", "acmmp_device_count",
                         "acmmp_depth_from_plane_param", "acmmp_comm_destroy", "acmmp_fusion_last_error",
-                        "acmmp_fusion_destroy"):
+                        "acmmp_fusion_destroy", "acmmp_image_cache_destroy"):
             fn.restype = i32
     L.acmmp_depth_from_plane_param.restype = C.c_float
     L.acmmp_fusion_last_error.restype = C.c_char_p
+    L.acmmp_image_cache_destroy.restype = None
     _lib = L
     return L
 
@@ -137,6 +143,35 @@ def device_count() -> int:
 
 def _p(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class ImageCache:
+    """Prepared source images (padded fp32 + binary16) shared by the contexts of one GPU, keyed by the
+    caller (acmmp_image_cache_*).  Safe to close before the contexts that used it."""
+
+    def __init__(self, device: int = 0, budget_bytes: int = 0):
+        self.L = load_library()
+        h = C.c_void_p()
+        rc = self.L.acmmp_image_cache_create(device, C.c_size_t(budget_bytes), C.byref(h))
+        if rc != 0:
+            raise AcmmpError(f"acmmp_image_cache_create: {self.L.acmmp_status_str(rc).decode()}")
+        self.h, self.device = h, device
+
+    def stats(self) -> dict:
+        out = np.zeros(5, np.uint64)
+        _host_check(self.L.acmmp_image_cache_stats(self.h, _p(out)), "image_cache_stats")
+        return dict(zip(("hits", "misses", "bytes", "entries", "evictions"), (int(x) for x in out)))
+
+    def close(self):
+        if self.h:
+            self.L.acmmp_image_cache_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:                                            # noqa: BLE001
+            pass
 
 
 class Context:
@@ -215,14 +250,23 @@ class Context:
         self._check(self.L.acmmp_upload_views(self.h, n, C.cast(ptrs, C.c_void_p), None, _p(cams)), "upload_views")
         self.N, self.H, self.W = n, imgs[0].shape[0], imgs[0].shape[1]
 
-    def upload_views_device(self, bufs, cameras):
-        """bufs: DeviceBuffer images (index 0 = reference) on this context's GPU."""
+    def upload_views_device(self, bufs, cameras, cache: "ImageCache | None" = None, keys=None):
+        """bufs: DeviceBuffer images (index 0 = reference) on this context's GPU.  With an ImageCache and
+        one nonzero content key per view (the caller's promise that equal keys mean equal pixels), views
+        the cache already holds are neither copied nor converted again (acmmp_upload_views_keyed)."""
         cams = np.frombuffer(np.ascontiguousarray(cameras, dtype=CAMERA_DTYPE).tobytes(), CAMERA_DTYPE).copy()
         self._check_view_shapes([tuple(b.shape[:2]) for b in bufs], cams)
         n = len(bufs)
         ptrs = (C.c_void_p * n)(*[b.ptr for b in bufs])
-        self._check(self.L.acmmp_upload_views_device(self.h, n, C.cast(ptrs, C.c_void_p), None, _p(cams)),
-                    "upload_views_device")
+        if cache is not None:
+            k = np.ascontiguousarray(keys, np.uint64)
+            if k.shape != (n,):
+                raise ValueError(f"upload_views_device: {n} views but keys of shape {k.shape}")
+            self._check(self.L.acmmp_upload_views_keyed(self.h, cache.h, n, _p(k), C.cast(ptrs, C.c_void_p), None,
+                                                        _p(cams), 1), "upload_views_keyed")
+        else:
+            self._check(self.L.acmmp_upload_views_device(self.h, n, C.cast(ptrs, C.c_void_p), None, _p(cams)),
+                        "upload_views_device")
         self.N, self.H, self.W = n, bufs[0].shape[0], bufs[0].shape[1]
 
     def upload_depths(self, depths):

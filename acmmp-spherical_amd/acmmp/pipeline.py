@@ -362,6 +362,9 @@ class Pipeline:
         self.overlap = slots if (gpu and slots > 1) else 0
         self._extra_engines = []
         self._math = math
+        # prepared (padded + binary16) images of every (view, scale), shared by this pipeline's contexts:
+        # each is prepared once, not once per problem that reads it
+        self.image_cache = capi.ImageCache(device, int(os.environ.get("ACMMP_IMAGE_CACHE_BYTES", 0))) if gpu else None
         if gpu:
             self.log(f"engine math: {self.engine.math()}")
 
@@ -380,11 +383,14 @@ class Pipeline:
         return self._extra_engines[0] if self._extra_engines else None
 
     def close(self):
-        """Release the engine context(s) this pipeline created or was given."""
+        """Release the engine context(s) this pipeline created or was given, and its image cache."""
         for e in self._extra_engines + [self.engine]:
             if e is not None and hasattr(e, "close"):
                 e.close()
         self._extra_engines = []
+        if self.image_cache is not None:
+            self.image_cache.close()
+            self.image_cache = None
 
     # -- sharding
     def owner(self, i: int) -> int:
@@ -498,7 +504,11 @@ class Pipeline:
                 b.upload(img)
                 self._scaled_dev[key] = b
             bufs.append(b)
-        e.upload_views_device(bufs, cams)
+        if self.image_cache is not None and isinstance(e, capi.Context):
+            keys = [((vid + 1) << 24) | size for vid, size in self._keys]
+            e.upload_views_device(bufs, cams, cache=self.image_cache, keys=keys)
+        else:
+            e.upload_views_device(bufs, cams)
 
     def _pass_overlapped(self, hier, log):
         """A planar pass over `self.overlap` engine contexts on the GPU: view k's second half (host planar

@@ -13,7 +13,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "engine.h"
@@ -26,6 +28,29 @@ static_assert(sizeof(acmmp_params) == 68, "PatchMatchParams layout (ACMMP.h:32-5
 static_assert(offsetof(acmmp_params, scaled_cols) == 52, "PatchMatchParams layout");
 static_assert(offsetof(acmmp_params, geom_consistency) == 60, "PatchMatchParams layout");
 
+// Padded fp32 + row-pair binary16 source images shared by contexts on one GPU, keyed by the caller's
+// content key (acmmp_upload_views_keyed): a pipeline prepares each (view, scale) once instead of once
+// per problem that reads it.  Entries a context's current problem uses are pinned until its next upload.
+struct acmmp_image_cache {
+    struct Entry {
+        int W = 0, H = 0;
+        float* img = nullptr;            // padded (W + 2) x (H + 2) fp32
+        uint32_t* img16 = nullptr;       // row-pair binary16 copy, null when some texel is not exact
+        bool f16_checked = false;        // the binary16 conversion was attempted (img16 null: inexact)
+        size_t bytes = 0;
+        int pins = 0;
+        uint64_t used = 0;               // LRU clock
+    };
+    int device = 0;
+    size_t budget = 0;                   // soft limit in bytes, 0 = none
+    int refs = 1;                        // the creator's + one per context pinning entries
+    std::mutex mu;
+    std::unordered_map<uint64_t, Entry> map;
+    size_t bytes = 0;
+    uint64_t clock = 0;
+    unsigned long long hits = 0, misses = 0, evictions = 0;
+};
+
 struct acmmp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -37,12 +62,19 @@ struct acmmp_ctx {
     std::vector<acmmp_camera> cams;
     std::vector<DevCam> dcams;
     DevCam* d_cams = nullptr;
-    float* d_img = nullptr;
-    uint16_t* d_img16 = nullptr;     // binary16 copy of d_img (null when some texel is not exact)
+    float* d_img = nullptr;          // padded fp32 images of the views not in an image cache
+    uint32_t* d_img16 = nullptr;     // their row-pair binary16 copies
     size_t img_cap = 0, img16_cap = 0;  // texels the two image allocations hold (grow-only)
     char* d_stage = nullptr;         // upload staging for all of a problem's images (grow-only)
     size_t stage_cap = 0;
-    int* d_flag = nullptr;           // k_to_f16's inexact flag
+    int* d_flag = nullptr;           // k_to_f16_pairs' inexact flags, one per view
+    size_t flag_cap = 0;
+    bool tex16 = false;              // every view of the problem has an exact binary16 copy
+    acmmp_image_cache* pin_cache = nullptr;   // entries the current problem pins
+    std::vector<uint64_t> pinned;
+    std::vector<float*> orphans;     // keyed images another context cached first (freed at the next upload)
+    std::vector<uint32_t*> orphans16;
+    size_t cams_cap = 0;
 
     float* d_dep = nullptr;
     bool has_depths = false;
@@ -181,7 +213,8 @@ void acmmp::set_relative_frame(DevCam& d, const acmmp_camera& ref, const acmmp_c
         for (int k = 0; k < 3; ++k) {
             const double v = pin ? double(s.K[3 * r]) * M[k] + double(s.K[3 * r + 1]) * M[3 + k] + double(s.K[3 * r + 2]) * M[6 + k]
                                  : M[3 * r + k];
-            d.FR[3 * r + k] = static_cast<float>(v);
+            if (r < 2) d.FRxy[2 * k + r] = static_cast<float>(v);   // rows 0, 1 interleaved (packed x, y)
+            else d.FRz[k] = static_cast<float>(v);
         }
         const double v = pin ? double(s.K[3 * r]) * b[0] + double(s.K[3 * r + 1]) * b[1] + double(s.K[3 * r + 2]) * b[2] : b[r];
         d.Ft[r] = static_cast<float>(v);
@@ -240,10 +273,13 @@ acmmp_status acmmp_create(int device, acmmp_ctx** out) {
     return ACMMP_OK;
 }
 
+static void unpin_views(acmmp_ctx* c);
+
 void acmmp_destroy(acmmp_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    unpin_views(c);
     dfree(c->d_cams); dfree(c->d_img); dfree(c->d_img16); dfree(c->d_dep); dfree(c->d_dirs);
     dfree(c->d_stage); dfree(c->d_flag);
     dfree(c->d_sph_row); dfree(c->d_sph_col); dfree(c->d_spatial);
@@ -281,23 +317,115 @@ acmmp_status acmmp_set_params(acmmp_ctx* c, const acmmp_params* p) {
 
 
 static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* images, const size_t* pitch_bytes,
-                                      const acmmp_camera* cams, bool device_src);
+                                      const acmmp_camera* cams, bool device_src, acmmp_image_cache* cache,
+                                      const uint64_t* keys);
 
 acmmp_status acmmp_upload_views(acmmp_ctx* c, int n, const float* const* images, const size_t* pitch_bytes,
                                 const acmmp_camera* cams) {
-    return upload_views_impl(c, n, images, pitch_bytes, cams, false);
+    return upload_views_impl(c, n, images, pitch_bytes, cams, false, nullptr, nullptr);
 }
 
 acmmp_status acmmp_upload_views_device(acmmp_ctx* c, int n, const float* const* dev_images, const size_t* pitch_bytes,
                                        const acmmp_camera* cams) {
-    return upload_views_impl(c, n, dev_images, pitch_bytes, cams, true);
+    return upload_views_impl(c, n, dev_images, pitch_bytes, cams, true, nullptr, nullptr);
+}
+
+acmmp_status acmmp_upload_views_keyed(acmmp_ctx* c, acmmp_image_cache* cache, int n, const uint64_t* keys,
+                                      const float* const* images, const size_t* pitch_bytes, const acmmp_camera* cams,
+                                      int device_src) {
+    if (c && cache && cache->device != c->device)
+        return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "image cache belongs to another device");
+    return upload_views_impl(c, n, images, pitch_bytes, cams, device_src != 0, cache, keys);
+}
+
+acmmp_status acmmp_image_cache_create(int device, size_t budget_bytes, acmmp_image_cache** out) {
+    if (!out) return ACMMP_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return ACMMP_ERR_NO_DEVICE;
+    if (device < 0 || device >= n) return ACMMP_ERR_INVALID_ARGUMENT;
+    acmmp_image_cache* k = new acmmp_image_cache();
+    k->device = device;
+    k->budget = budget_bytes;
+    *out = k;
+    return ACMMP_OK;
 }
 
 }  // extern "C"
 
+// Drop one reference; the last one frees the cache (contexts that still pin entries keep it alive
+// until their next upload or their destruction).
+static void cache_release(acmmp_image_cache* k) {
+    bool last;
+    {
+        std::lock_guard<std::mutex> lk(k->mu);
+        last = --k->refs == 0;
+    }
+    if (!last) return;
+    (void)hipSetDevice(k->device);
+    for (auto& kv : k->map) {
+        dfree(kv.second.img);
+        dfree(kv.second.img16);
+    }
+    delete k;
+}
+
+extern "C" {
+
+void acmmp_image_cache_destroy(acmmp_image_cache* k) {
+    if (k) cache_release(k);
+}
+
+acmmp_status acmmp_image_cache_stats(acmmp_image_cache* k, unsigned long long out[5]) {
+    if (!k || !out) return ACMMP_ERR_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(k->mu);
+    out[0] = k->hits; out[1] = k->misses; out[2] = k->bytes; out[3] = k->map.size(); out[4] = k->evictions;
+    return ACMMP_OK;
+}
+
+}  // extern "C"
+
+static void unpin_views(acmmp_ctx* c) {
+    for (auto& p : c->orphans) dfree(p);
+    for (auto& p : c->orphans16) dfree(p);
+    c->orphans.clear();
+    c->orphans16.clear();
+    if (!c->pin_cache) return;
+    {
+        std::lock_guard<std::mutex> lk(c->pin_cache->mu);
+        for (uint64_t key : c->pinned) {
+            auto it = c->pin_cache->map.find(key);
+            if (it != c->pin_cache->map.end() && it->second.pins > 0) --it->second.pins;
+        }
+    }
+    c->pinned.clear();
+    acmmp_image_cache* k = c->pin_cache;
+    c->pin_cache = nullptr;
+    cache_release(k);
+}
+
+// Least-recently used unpinned entries go first; the budget is soft (pinned entries stay).
+static void evict_over_budget(acmmp_image_cache* k) {
+    if (k->budget == 0) return;
+    while (k->bytes > k->budget) {
+        auto victim = k->map.end();
+        for (auto it = k->map.begin(); it != k->map.end(); ++it)
+            if (it->second.pins == 0 && (victim == k->map.end() || it->second.used < victim->second.used)) victim = it;
+        if (victim == k->map.end()) return;
+        dfree(victim->second.img);
+        dfree(victim->second.img16);
+        k->bytes -= victim->second.bytes;
+        k->map.erase(victim);
+        ++k->evictions;
+    }
+}
+
 // Host images go through one staging buffer; device images are padded straight from their buffers.
+// Views found in `cache` (same key and size) reuse its padded and binary16 copies; the others are
+// padded, converted and checked here (one flag read and one stream sync per call, for all of them).
 static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* images, const size_t* pitch_bytes,
-                                      const acmmp_camera* cams, bool device_src) {
+                                      const acmmp_camera* cams, bool device_src, acmmp_image_cache* cache,
+                                      const uint64_t* keys) {
     if (!c || !images || !cams) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
     if (n < 2 || n > kMaxViews + 1) return fail(c, ACMMP_ERR_UNSUPPORTED, "need 2..33 images");
     for (int i = 0; i < n; ++i) {
@@ -311,6 +439,8 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
             return fail(c, ACMMP_ERR_UNSUPPORTED, "mixed camera models in one problem are not supported");
     }
     HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));          // the previous problem's kernels read the old images
+    unpin_views(c);
     const bool resized = (c->W != cams[0].width || c->H != cams[0].height);
     // a new problem: the previous problem's prior / scaled state no longer applies (the reference
     // builds a fresh ACMMP object per ProcessProblem, main.cpp:80)
@@ -322,85 +452,156 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
     c->model = cams[0].model;
     c->cams.assign(cams, cams + n);
     c->dirs_R = -1;
+    // binary16 copies for the NCC fetches when they hold the same values (8-bit images always do): half
+    // the bytes per footprint, so twice the views fit a cache level.  ACMMP_TEX16=0 in the
+    // environment keeps the fp32 fetches (A/B switch; identical results).
+    const char* tex16_env = std::getenv("ACMMP_TEX16");
+    const bool want16 = !(tex16_env && tex16_env[0] == '0');
 
-    // padded images in one allocation
-    std::vector<long long> off(n);
+    std::vector<float*> base(n, nullptr);
+    std::vector<uint32_t*> base16(n, nullptr);
+    std::vector<int> miss;                               // views padded / converted by this call
+    std::vector<bool> keyed(n, false);
+    if (cache && keys) {
+        std::lock_guard<std::mutex> lk(cache->mu);
+        ++cache->refs;                                    // released by unpin_views
+        for (int i = 0; i < n; ++i) {
+            if (!keys[i]) continue;
+            auto it = cache->map.find(keys[i]);
+            if (it != cache->map.end() && it->second.W == cams[i].width && it->second.H == cams[i].height &&
+                (it->second.f16_checked || !want16)) {
+                base[i] = it->second.img;
+                base16[i] = want16 ? it->second.img16 : nullptr;
+                ++it->second.pins;
+                it->second.used = ++cache->clock;
+                c->pinned.push_back(keys[i]);
+                ++cache->hits;
+            } else {
+                keyed[i] = it == cache->map.end() || it->second.pins == 0;   // (re)insert this key
+                ++cache->misses;
+            }
+        }
+        c->pin_cache = cache;
+    }
+    std::vector<bool> is_miss(n, false);
+    for (int i = 0; i < n; ++i) if (!base[i]) { miss.push_back(i); is_miss[i] = true; }
+
+    // private (unkeyed) views share the context's grow-only allocation; keyed misses get their own
+    std::vector<long long> off(n, 0);
     long long total = 0;
-    for (int i = 0; i < n; ++i) {
-        off[i] = total;                                 // base = padded texel (-1,-1)
+    for (int i : miss) {
+        if (keyed[i]) continue;
+        off[i] = total;                                  // base = padded texel (-1,-1)
         total += static_cast<long long>(cams[i].width + 2) * (cams[i].height + 2);
         total = (total + 63) & ~63LL;
     }
-    // allocations are kept across uploads (a pipeline uploads every problem of every pass); all
-    // images go through one staging buffer, copies and padding kernels back to back on the stream
-    HIP_TRY(c, dreserve(c->d_img, c->img_cap, static_cast<size_t>(total)));
-    HIP_TRY(c, hipMemsetAsync(c->d_img, 0, sizeof(float) * static_cast<size_t>(total), c->stream));  // gaps between views
-    std::vector<size_t> soff(n + 1, 0);
-    for (int i = 0; i < n; ++i) {
-        const size_t rowb = sizeof(float) * cams[i].width;
-        const size_t pb = pitch_bytes ? pitch_bytes[i] : rowb;
-        soff[i + 1] = soff[i] + ((pb * (cams[i].height - 1) + rowb + 255) & ~static_cast<size_t>(255));
+    if (total > 0) {
+        HIP_TRY(c, dreserve(c->d_img, c->img_cap, static_cast<size_t>(total)));
+        if (want16) HIP_TRY(c, dreserve(c->d_img16, c->img16_cap, static_cast<size_t>(total)));
     }
-    if (!device_src) HIP_TRY(c, dreserve(c->d_stage, c->stage_cap, soff[n]));
-    for (int i = 0; i < n; ++i) {
-        const size_t rowb = sizeof(float) * cams[i].width;
-        const size_t pb = pitch_bytes ? pitch_bytes[i] : rowb;
-        const size_t bytes = pb * (cams[i].height - 1) + rowb;
-        const float* src = images[i];
-        if (!device_src) {
-            float* staging = reinterpret_cast<float*>(c->d_stage + soff[i]);
-            HIP_TRY(c, hipMemcpyAsync(staging, images[i], bytes, hipMemcpyHostToDevice, c->stream));
-            src = staging;
-        }
-        HIP_TRY(c, launch_pad_image(src, pb / sizeof(float), cams[i].width, cams[i].height, c->d_img + off[i],
-                                    cams[i].width + 2, c->stream));
-    }
-
-    // binary16 copy for the NCC fetches when it holds the same values (8-bit images always do):
-    // half the bytes per footprint, so twice the views fit a cache level.
-    // ACMMP_TEX16=0 in the environment keeps the fp32 fetches (A/B switch; identical results).
-    const char* tex16_env = std::getenv("ACMMP_TEX16");
-    if (!(tex16_env && tex16_env[0] == '0')) {
-        // ACMMP_TEX_PAIRS builds keep the row-pair layout: 4 bytes per texel position, the same offsets
-        // as the fp32 images
-        const bool pairs = tex_pairs_layout() != 0;
-        HIP_TRY(c, dreserve(c->d_img16, c->img16_cap, static_cast<size_t>(total) * (pairs ? 2 : 1)));
-        if (!c->d_flag) HIP_TRY(c, dalloc(c->d_flag, 1));
-        int inexact = 0;
-        HIP_TRY(c, hipMemsetAsync(c->d_flag, 0, sizeof(int), c->stream));
-        if (pairs) {
-            for (int i = 0; i < n; ++i)
-                HIP_TRY(c, launch_to_f16_pairs(c->d_img + off[i], cams[i].width, cams[i].height,
-                                               reinterpret_cast<uint32_t*>(c->d_img16) + off[i], c->d_flag, c->stream));
+    std::vector<float*> own(n, nullptr);
+    std::vector<uint32_t*> own16(n, nullptr);
+    for (int i : miss) {
+        if (keyed[i]) {
+            const size_t texels = static_cast<size_t>(cams[i].width + 2) * (cams[i].height + 2);
+            HIP_TRY(c, dalloc(own[i], texels));
+            if (want16) HIP_TRY(c, dalloc(own16[i], texels));
+            base[i] = own[i];
+            base16[i] = own16[i];
         } else {
-            HIP_TRY(c, launch_to_f16(c->d_img, total, c->d_img16, c->d_flag, c->stream));
+            base[i] = c->d_img + off[i];
+            base16[i] = want16 ? c->d_img16 + off[i] : nullptr;
         }
-        HIP_TRY(c, hipMemcpyAsync(&inexact, c->d_flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-        if (inexact) { dfree(c->d_img16); c->img16_cap = 0; }
-    } else {
-        dfree(c->d_img16);
-        c->img16_cap = 0;
     }
-    HIP_TRY(c, hipStreamSynchronize(c->stream));          // staging and padding done before returning
+    if (!miss.empty()) {
+        std::vector<size_t> soff(n + 1, 0);
+        for (int i = 0; i < n; ++i) {
+            const size_t rowb = sizeof(float) * cams[i].width;
+            const size_t pb = pitch_bytes ? pitch_bytes[i] : rowb;
+            soff[i + 1] = soff[i] + (is_miss[i] ? ((pb * (cams[i].height - 1) + rowb + 255) & ~static_cast<size_t>(255)) : 0);
+        }
+        if (!device_src) HIP_TRY(c, dreserve(c->d_stage, c->stage_cap, soff[n]));
+        if (want16) {
+            HIP_TRY(c, dreserve(c->d_flag, c->flag_cap, static_cast<size_t>(n)));
+            HIP_TRY(c, hipMemsetAsync(c->d_flag, 0, sizeof(int) * n, c->stream));
+        }
+        for (int i : miss) {
+            const size_t rowb = sizeof(float) * cams[i].width;
+            const size_t pb = pitch_bytes ? pitch_bytes[i] : rowb;
+            const size_t bytes = pb * (cams[i].height - 1) + rowb;
+            const float* src = images[i];
+            if (!device_src) {
+                float* staging = reinterpret_cast<float*>(c->d_stage + soff[i]);
+                HIP_TRY(c, hipMemcpyAsync(staging, images[i], bytes, hipMemcpyHostToDevice, c->stream));
+                src = staging;
+            }
+            HIP_TRY(c, launch_pad_image(src, pb / sizeof(float), cams[i].width, cams[i].height, base[i],
+                                        cams[i].width + 2, c->stream));
+            if (want16)
+                HIP_TRY(c, launch_to_f16_pairs(base[i], cams[i].width, cams[i].height, base16[i], c->d_flag + i,
+                                               c->stream));
+        }
+        std::vector<int> inexact(n, 0);
+        if (want16) HIP_TRY(c, hipMemcpyAsync(inexact.data(), c->d_flag, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));      // staging, padding and flags done before returning
+        for (int i : miss) {
+            if (inexact[i]) {
+                if (keyed[i]) dfree(own16[i]);
+                base16[i] = nullptr;
+            }
+        }
+        if (cache && keys) {
+            std::lock_guard<std::mutex> lk(cache->mu);
+            for (int i : miss) {
+                if (!keyed[i]) continue;
+                auto it = cache->map.find(keys[i]);
+                if (it != cache->map.end()) {
+                    if (it->second.pins > 0) {              // another context inserted it meanwhile: use ours privately
+                        keyed[i] = false;
+                        continue;
+                    }
+                    dfree(it->second.img);
+                    dfree(it->second.img16);
+                    cache->bytes -= it->second.bytes;
+                    cache->map.erase(it);
+                }
+                acmmp_image_cache::Entry e;
+                e.W = cams[i].width; e.H = cams[i].height;
+                e.img = own[i]; e.img16 = own16[i];
+                e.f16_checked = want16;
+                e.bytes = sizeof(float) * static_cast<size_t>(e.W + 2) * (e.H + 2) * (own16[i] ? 2 : 1);
+                e.pins = 1;
+                e.used = ++cache->clock;
+                cache->bytes += e.bytes;
+                cache->map.emplace(keys[i], e);
+                c->pinned.push_back(keys[i]);
+                own[i] = nullptr; own16[i] = nullptr;      // owned by the cache now
+            }
+            evict_over_budget(cache);
+        }
+        // keyed misses that could not enter the cache stay with this context until its next upload
+        for (int i : miss) {
+            if (own[i]) c->orphans.push_back(own[i]);
+            if (own16[i]) c->orphans16.push_back(own16[i]);
+        }
+    }
+    c->tex16 = want16;
+    for (int i = 0; i < n; ++i) c->tex16 = c->tex16 && base16[i] != nullptr;
 
     c->dcams.assign(n, DevCam{});
     for (int i = 0; i < n; ++i) {
         const acmmp_camera& s = cams[i];
         DevCam& d = c->dcams[i];
         d = make_devcam(s);
-        d.img_off = off[i];
-        d.img_base = c->d_img + off[i];
+        d.img_base = base[i];
         d.img_bytes = static_cast<int>(4LL * (s.width + 2) * (s.height + 2));
-        const int tp = tex_pairs_layout() ? 2 : 1;
-        d.img16_base = c->d_img16 ? c->d_img16 + tp * off[i] : nullptr;
-        d.img16_bytes = static_cast<int>(2LL * tp * (s.width + 2) * (s.height + 2));
-        d.pitch2 = 2 * (s.width + 2);
+        d.img16_base = c->tex16 ? reinterpret_cast<const uint16_t*>(base16[i]) : nullptr;
+        d.img16_bytes = static_cast<int>(4LL * (s.width + 2) * (s.height + 2));
         d.dep_off = 0; d.dep_w = 1; d.dep_h = 1;
         set_relative_frame(d, cams[0], s);
     }
-    HIP_TRY(c, dalloc(c->d_cams, static_cast<size_t>(n)));
-    HIP_TRY(c, hipMemcpy(c->d_cams, c->dcams.data(), sizeof(DevCam) * n, hipMemcpyHostToDevice));
+    HIP_TRY(c, dreserve(c->d_cams, c->cams_cap, static_cast<size_t>(n)));
+    HIP_TRY(c, hipMemcpyAsync(c->d_cams, c->dcams.data(), sizeof(DevCam) * n, hipMemcpyHostToDevice, c->stream));
     c->has_depths = false;
 
     if (resized || !c->d_planes_rm) {
@@ -410,9 +611,9 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
         HIP_TRY(c, dalloc(c->d_costs_rm, P));
         HIP_TRY(c, dalloc(c->d_pre, P));
         HIP_TRY(c, dalloc(c->d_sel_rm, P));
-        HIP_TRY(c, hipMemset(c->d_planes_rm, 0, sizeof(float4) * P));
-        HIP_TRY(c, hipMemset(c->d_costs_rm, 0, sizeof(float) * P));
-        HIP_TRY(c, hipMemset(c->d_sel_rm, 0, sizeof(uint32_t) * P));
+        HIP_TRY(c, hipMemsetAsync(c->d_planes_rm, 0, sizeof(float4) * P, c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->d_costs_rm, 0, sizeof(float) * P, c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->d_sel_rm, 0, sizeof(uint32_t) * P, c->stream));
         for (int k = 0; k < 2; ++k) {
             for (int b = 0; b < 2; ++b) {
                 HIP_TRY(c, dalloc(c->d_plane_cs[k][b], Pc));
@@ -671,8 +872,7 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
         c->scratch_bytes = off[12];
     }
     kp.cams = c->d_cams;
-    kp.img = c->d_img;
-    kp.tex16 = c->d_img16 != nullptr;
+    kp.tex16 = c->tex16;
     kp.fast = c->math == ACMMP_MATH_FAST;
     kp.dep = c->d_dep;
     kp.dirs = c->d_dirs;
@@ -965,8 +1165,8 @@ acmmp_status acmmp_last_work(const acmmp_ctx* c, unsigned long long* evaluated, 
 }
 
 int acmmp_texel_bytes(const acmmp_ctx* c) {
-    if (!c || !c->d_img) return 0;
-    return c->d_img16 ? 2 : 4;
+    if (!c || c->N == 0) return 0;
+    return c->tex16 ? 2 : 4;
 }
 
 acmmp_status acmmp_last_kernel_timing(const acmmp_ctx* c, float ms[4], int launches[4]) {

@@ -34,11 +34,14 @@ struct DevCam {
     // The fast projection works in the reference camera's frame: a source point is FR q + Ft for the
     // camera-frame point q = depth * ray of the reference pixel, FR = K R R0^T and Ft = K (R C0 + t)
     // (K = identity for SPHERE; R0, C0: the problem's reference camera, rounded once from doubles).
-    float FR[9], Ft[3];
+    float FRxy[6];                  // FR rows 0 and 1 interleaved: FR00 FR10 FR01 FR11 FR02 FR12
+    float FRz[3];                   // FR row 2
+    float Ft[3];
     float fkx, fky;                 // SPHERE: W / (2 pi), H / pi (fast mode)
     float cx, cy;                   // SPHERE params[1], params[2]
-    // binary16 copy of the padded image (same layout, 2 B per texel), present when every texel of
-    // every view is exactly representable (8-bit images are): half the cache footprint, same values
+    // row-pair binary16 copy of the padded image (word (X, Y) = (t(X, Y), t(X, Y + 1))), present when
+    // every texel of every view is exactly representable (8-bit images are): one 8-byte load per
+    // bilinear footprint, same values
     const uint16_t* img16_base;
     int img16_bytes;
     float invW;                     // 1/W             (SPHERE longitude wrap)
@@ -54,13 +57,11 @@ struct DevCam {
     float inv_fx, inv_fy;           // 1/K[0], 1/K[4]  (pinhole world point)
     float Hf;
     float C[3];                     // camera centre -(R^T t), computed like ACMMP.cu:592-594
-    long long img_off;              // float offset of padded texel (-1,-1)
     long long dep_off;              // float offset of the geom depth map (row-major)
     int dep_w, dep_h;
     int img_bytes;                  // bytes of the padded image (buffer descriptor range)
     int Hm1;                        // H - 1 (texel clamp)
     const float* img_base;          // device address of padded texel (-1,-1) (buffer descriptor base)
-    int pitch2;                     // bytes per padded binary16 row
 };
 
 // Per-pixel state handed from k_select to k_eval_ref / k_finish (80 bytes).
@@ -95,7 +96,6 @@ struct KParams {
     int sw, sh;
     uint32_t seed_lo, seed_hi;
     const DevCam* cams;
-    const float* img;
     const float* dep;
     const float4* dirs;             // PINHOLE ray table, (W+2R) x (H+2R)
     const float2* sph_row;          // SPHERE (sin, cos) latitude, rows -R .. H+R-1
@@ -185,12 +185,10 @@ hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int s
                       float* out, hipStream_t s);
 hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,
                         float* out, hipStream_t s);
-// Padded fp32 images -> binary16 copy; *inexact (device int, pre-zeroed) is set when a texel is not
-// exactly representable as a normal binary16 number or zero.
-hipError_t launch_to_f16(const float* src, long long n, uint16_t* dst, int* inexact, hipStream_t s);
-// Row-pair binary16 copy of one padded view (W + 2) x (H + 2) (kernels.hip ACMMP_TEX_PAIRS layout).
+// Row-pair binary16 copy of one padded view (W + 2) x (H + 2) (DevCam::img16_base layout); *inexact
+// (device int, pre-zeroed) is set when a texel is not exactly representable as a normal binary16
+// number or zero.
 hipError_t launch_to_f16_pairs(const float* src, int W, int H, uint32_t* dst, int* inexact, hipStream_t s);
-int tex_pairs_layout();
 hipError_t launch_pad_image(const float* src, size_t pitch_floats, int W, int H, float* dst, int dst_pitch,
                             hipStream_t s);
 

@@ -33,6 +33,13 @@
 
 namespace acmmp {
 
+// Two-lane f32 vectors: arithmetic on them issues as the packed VALU forms (v_pk_fma_f32 / v_pk_mul_f32 /
+// v_pk_add_f32: two IEEE single-precision operations per lane in one issue slot, scripts/micro/pk_rate.hip:
+// 123 TFLOP/s against 71 for v_fma_f32), with scalar operands broadcast through op_sel.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 splat2(float x) { return (f32x2){x, x}; }
+
 // ------------------------------------------------------------------ RNG
 
 __device__ __forceinline__ uint4 philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
@@ -257,22 +264,11 @@ __device__ __forceinline__ float depth_from_plane(float4 ph, float4 d) {
 // returns 0 there, this returns NaN and the sample's cost is 2.0).  Not bit-identical to the
 // oracle: parity is the tolerance of SURVEY.md §8c (tests/test_gpu_fastmath.py).
 
-#ifndef ACMMP_FM_GUARD
-#define ACMMP_FM_GUARD 0                    // fast mode: the |t| < 1e-6 test costs 3 VALU per view-sample
-#endif                                      // (r02 A/B profiles/r02_micro_ab.txt: metric +2%, C3 +1.8%)
 // Chunks whose VB views are all present compile without per-view guards (one basic block per sample):
-// pinhole +17% at C2 (V = 10: its 8-view chunk).  SPHERE (ACMMP_FULL_CHUNK_SPH: 0 never, 1 always,
-// 2 = chunks of at most 2 views outside k_eval_nb): k_eval_nb's 4-view chunks -1..-3% (longer live
-// ranges), k_eval_ref's 2-view chunks at V = 15 +4.7% (r02 A/B profiles/r02_full_chunk_ab.txt)
-#ifndef ACMMP_FULL_CHUNK_PIN
-#define ACMMP_FULL_CHUNK_PIN 1
-#endif
-#ifndef ACMMP_VIEW_BARRIER
-#define ACMMP_VIEW_BARRIER 1
-#endif
-#ifndef ACMMP_FULL_CHUNK_SPH
-#define ACMMP_FULL_CHUNK_SPH 2
-#endif
+// every pinhole chunk (+17% at C2, V = 10: its 8-view chunk) and SPHERE chunks of at most 2 views
+// (k_eval_ref's 2-view chunks at V = 15 +4.7%; SPHERE's 4-view k_eval_nb chunks lose 1-3% that way,
+// longer live ranges -- r02 A/B profiles/r02_full_chunk_ab.txt).  The fast mode has no |t| < 1e-6 test
+// per view-sample (3 VALU; r02 A/B profiles/r02_micro_ab.txt: metric +2%, C3 +1.8%).
 
 // atan(t) on [0, 1]: t + t^3 P(t^2), 7-term minimax, max |error| 1.1e-7 rad
 __device__ __forceinline__ float atan_core_fast(float t) {
@@ -287,46 +283,58 @@ __device__ __forceinline__ float atan_core_fast(float t) {
     return fmaf(t * z, p, t);
 }
 
+// The same for two arguments at once, in packed VALU operations.
+__device__ __forceinline__ f32x2 atan_core_fast2(f32x2 t) {
+    const f32x2 z = t * t;
+    f32x2 p = splat2(-0.004355291370302439f);
+    p = pk_fma(p, z, splat2(0.023039722815155983f));
+    p = pk_fma(p, z, splat2(-0.05777300149202347f));
+    p = pk_fma(p, z, splat2(0.09794192016124725f));
+    p = pk_fma(p, z, splat2(-0.139765664935112f));
+    p = pk_fma(p, z, splat2(0.19962701201438904f));
+    p = pk_fma(p, z, splat2(-0.3333165943622589f));
+    return pk_fma(t * z, p, t);
+}
+
 // P: the sample's point in the REFERENCE camera's frame (depth * ray); FR / Ft map it into the source
-// camera (DevCam::FR, set per problem), so no world point is formed per sample.
+// camera (DevCam::FRxy / FRz / Ft, set per problem), so no world point is formed per sample.  Rows 0
+// and 1 of FR are interleaved in DevCam so (x, y) of the mapped point is one packed fma chain (the same
+// fma order per row as three separate rows), with the pair of constants as one SGPR pair.
 // ft: the translation Ft, from the camera (nullptr) or from registers the caller holds (a VOP3 fma reads
 // one SGPR, so a translation in SGPRs costs a move per row and view-sample)
 template <int MODEL, typename Cam>
-__device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float& oy, const float* ft = nullptr,
-                                             const float* cc = nullptr) {
+__device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float& oy, const float* ft = nullptr) {
+    const f32x2 fxy = ft ? (f32x2){ft[0], ft[1]} : (f32x2){c.Ft[0], c.Ft[1]};
+    const float fz = ft ? ft[2] : c.Ft[2];
+    f32x2 t = pk_fma((f32x2){c.FRxy[0], c.FRxy[1]}, splat2(P.x), fxy);
+    t = pk_fma((f32x2){c.FRxy[2], c.FRxy[3]}, splat2(P.y), t);
+    t = pk_fma((f32x2){c.FRxy[4], c.FRxy[5]}, splat2(P.z), t);
+    const float tz = fmaf(c.FRz[2], P.z, fmaf(c.FRz[1], P.y, fmaf(c.FRz[0], P.x, fz)));
     if (MODEL == kSphere) {
-        const float f0 = ft ? ft[0] : c.Ft[0], f1 = ft ? ft[1] : c.Ft[1], f2 = ft ? ft[2] : c.Ft[2];
-        const float tx = fmaf(c.FR[2], P.z, fmaf(c.FR[1], P.y, fmaf(c.FR[0], P.x, f0)));
-        const float ty = fmaf(c.FR[5], P.z, fmaf(c.FR[4], P.y, fmaf(c.FR[3], P.x, f1)));
-        const float tz = fmaf(c.FR[8], P.z, fmaf(c.FR[7], P.y, fmaf(c.FR[6], P.x, f2)));
-        const float r2 = fmaf(tz, tz, fmaf(ty, ty, tx * tx));
-        // -latitude = asin(ty / |t|) (ProjectonCamera_cu :626-630)
-        const float s = __builtin_amdgcn_fmed3f(ty * __builtin_amdgcn_rsqf(r2), -1.0f, 1.0f);
-        const float a = fabsf(s);
-        const bool small = a <= 0.5f;
-        const float zl = fmaf(-0.5f, a, 0.5f);
-        const float cz = det_asin_core(small ? a : __builtin_amdgcn_sqrtf(zl), small ? a * a : zl);
-        const float neg_lat = copysignf(small ? cz : fmaf(-2.0f, cz, kPio2Hi), s);
-        // longitude = atan2(tx, tz) (:631)
-        const float ay = fabsf(tx), ax = fabsf(tz);
-        float r = atan_core_fast(fminf(ax, ay) * __builtin_amdgcn_rcpf(fmaxf(ax, ay)));
-        r = ay > ax ? kPio2Hi - r : r;
-        r = __builtin_bit_cast(int, tz) < 0 ? kPiHi - r : r;
-        const float lon = copysignf(r, tx);
-        ox = fmaf(lon, c.fkx, cc ? cc[0] : c.cx);
-        oy = fmaf(neg_lat, c.fky, cc ? cc[1] : c.cy);
-        // |t| < 1e-6 (:618-622): a sample on a source camera's centre.  ACMMP_FM_GUARD 0 drops the
-        // test: such a sample then projects to NaN and its view's cost is 2.0 (the NCC clamp) -- the
-        // reference's tex2D of (cx, cy) there is as meaningless, and no real geometry reaches it
-        if (ACMMP_FM_GUARD && r2 < 1e-12f) { ox = c.cx; oy = c.cy; }
+        // longitude = atan2(tx, tz) (ProjectonCamera_cu :631) and -latitude = asin(ty / |t|) (:626-630)
+        // = atan2(ty, hypot(tx, tz)): both through ONE packed atan over y = (tx, ty), x = (tz, h) -- the
+        // minimax atan of atan_core_fast (1.1e-7 rad) for the latitude too, in place of the asin
+        // polynomial with its range reduction and square root
+        const float h = __builtin_amdgcn_sqrtf(fmaf(tz, tz, t.x * t.x));
+        const f32x2 mn = (f32x2){min_abs(tz, t.x), min_abs(h, t.y)};
+        const f32x2 rc = (f32x2){__builtin_amdgcn_rcpf(max_abs(tz, t.x)), __builtin_amdgcn_rcpf(max_abs(h, t.y))};
+        f32x2 r = atan_core_fast2(mn * rc);
+        const f32x2 rq = splat2(kPio2Hi) - r;                          // |y| > |x|: pi/2 - atan(|x| / |y|)
+        r.x = fabsf(t.x) > fabsf(tz) ? rq.x : r.x;
+        r.y = fabsf(t.y) > h ? rq.y : r.y;
+        r.x = __builtin_bit_cast(int, tz) < 0 ? kPiHi - r.x : r.x;   // x < 0 (h >= 0 never is)
+        const f32x2 ang = (f32x2){copysignf(r.x, t.x), copysignf(r.y, t.y)};
+        const f32x2 o = pk_fma(ang, (f32x2){c.fkx, c.fky}, (f32x2){c.cx, c.cy});
+        ox = o.x;
+        oy = o.y;
+        // |t| < 1e-6 (:618-622), a sample on a source camera's centre, is not tested: such a sample
+        // projects to NaN and its view's cost is 2.0 (the NCC clamp) -- the reference's tex2D of
+        // (cx, cy) there is as meaningless, and no real geometry reaches it
     } else {
         // K (R_rel P + b) rows 0-1; the perspective divide by its row 2
-        const float hx = fmaf(c.FR[2], P.z, fmaf(c.FR[1], P.y, fmaf(c.FR[0], P.x, c.Ft[0])));
-        const float hy = fmaf(c.FR[5], P.z, fmaf(c.FR[4], P.y, fmaf(c.FR[3], P.x, c.Ft[1])));
-        const float tz = fmaf(c.FR[8], P.z, fmaf(c.FR[7], P.y, fmaf(c.FR[6], P.x, c.Ft[2])));
-        const float inv = __builtin_amdgcn_rcpf(tz);
-        ox = hx * inv;
-        oy = hy * inv;
+        const f32x2 o = t * splat2(__builtin_amdgcn_rcpf(tz));
+        ox = o.x;
+        oy = o.y;
     }
 }
 
@@ -412,7 +420,6 @@ struct Patch {
 };
 
 typedef float float2u __attribute__((ext_vector_type(2), aligned(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // tex2D(img, x+0.5, y+0.5) with fp32 bilinear weights and clamp addressing.  The one-texel
 // replicated border makes (ix, ix+1) valid for ix in [-1, W-1], which equals clamping both,
@@ -430,40 +437,33 @@ __device__ __forceinline__ float bilinear_pair(const float* img, int pitch, int 
     return fmaf(b, r1 - r0, r0);
 }
 
-#ifndef ACMMP_TEX_PAIRS
-#define ACMMP_TEX_PAIRS 1                   // the binary16 copy is row-pair interleaved: one 8-byte load per footprint
-                                            // (r02 A/B: +1% exact, +3.6% fast at the metric, neutral at C2/C3)
-#endif
-
 // The same fetch through a buffer descriptor of the view's padded image (32-bit texel offsets,
 // 24-bit multiply), split into issue (Tap) and use (lerp_tap) so a caller can put the loads of
 // several views in flight before consuming any.  SPHERE callers pass x already wrapped and y
 // clamped to [0, H-1] (never NaN), so y needs no clamp; x keeps clampi(f2i_sat(floor x), -1, W-1):
 // the float clamp below is the same map for every non-NaN value, and NaN -> 0 as f2i_sat does.
-#ifndef ACMMP_FRACT
-#define ACMMP_FRACT 1
-#endif
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 struct Tap {
     float a, b;
     f32x2 top, bot;
-    u32x2 pw;                       // ACMMP_TEX_PAIRS: the footprint's two row-pair words
+    u32x2 pw;                       // binary16: the footprint's two row-pair words
 };
 
 // ix = clampi(f2i_sat(floor x), -1, W-1), iy likewise (SPHERE: y already in [0, H-1], so iy = (int)floor y
 // >= 0); the footprint's top-left texel sits at byte (iy+1)*pitch4 + (ix+1)*4 of the padded image.
 // SPHERE moves the +1 row into the scalar offsets (top row soffset = pitch4, bottom = 2*pitch4).
 //
-// TEX = 1 reads the binary16 copy instead (DevCam::img16_base, same padded layout, 2 B per texel):
-// each row of the footprint is one 4-byte load at a 2-byte-aligned offset (the driver runs gfx9 in
-// unaligned-access mode) holding (t(ix), t(ix+1)) as (lo, hi) halves, kept raw in top.x / bot.x.
+// TEX = 1 reads the binary16 copy instead (DevCam::img16_base, row-pair layout: word (X, Y) =
+// (t(X, Y), t(X, Y + 1)), 4 B per texel position, the fp32 image's offsets): the footprint is the two
+// words at (ix + 1, iy + 1) and (ix + 2, iy + 1), one 8-byte load (r02 A/B against two 4-byte row
+// loads: +1% exact, +3.6% fast at the metric, neutral at C2/C3).
 template <int TEX, bool Y_IN_RANGE, typename Cam>
 __device__ __forceinline__ Tap fetch_tap(__amdgpu_buffer_rsrc_t rs, Cam& c, float x, float y) {
     const float fx = floorf(x), fy = floorf(y);
     Tap t;
     t.a = x - fx;
     t.b = y - fy;
-    if (TEX == 1 && ACMMP_TEX_PAIRS && ACMMP_FRACT) {
+    if (TEX == 1) {
         // the same footprint with v_fract_f32 / v_cvt_flr_i32_f32 (one instruction each instead of floor
         // + sub / floor + cvt).  fract(x) = min(x - floor(x), 1 - 2^-24) equals x - floor(x) unless x is
         // in (-2^-24, 0): a SPHERE x is wrapped (a negative one is sx - k W, a multiple of ulp(W) >= 2^-23)
@@ -480,35 +480,6 @@ __device__ __forceinline__ Tap fetch_tap(__amdgpu_buffer_rsrc_t rs, Cam& c, floa
         }
         return t;
     }
-    if (TEX == 1 && ACMMP_TEX_PAIRS) {
-        // row-pair layout: word (X, Y) = (t(X, Y), t(X, Y + 1)); the footprint is the two words at
-        // (ix + 1, iy + 1) and (ix + 2, iy + 1): one 8-byte load
-        const unsigned ix4 = (static_cast<unsigned>(clamp_m1(cvt_i32(fx), c.Wm1)) << 2) + 4u;
-        if (Y_IN_RANGE) {
-            const unsigned off = mad_u24(static_cast<unsigned>(cvt_i32(fy)), c.pitch4, ix4);
-            t.pw = __builtin_amdgcn_raw_buffer_load_b64(rs, off, c.pitch4, 0);
-        } else {
-            const unsigned off = mad_u24(static_cast<unsigned>(clamp_m1(cvt_i32(fy), c.Hm1) + 1), c.pitch4, ix4);
-            t.pw = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
-        }
-        return t;
-    }
-    if (TEX == 1) {
-        const unsigned ix2 = (static_cast<unsigned>(clamp_m1(cvt_i32(fx), c.Wm1)) << 1) + 2u;
-        unsigned top, bot;
-        if (Y_IN_RANGE) {
-            const unsigned off = mad_u24(static_cast<unsigned>(cvt_i32(fy)), c.pitch2, ix2);
-            top = __builtin_amdgcn_raw_buffer_load_b32(rs, off, c.pitch2, 0);
-            bot = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 2 * c.pitch2, 0);
-        } else {
-            const unsigned off = mad_u24(static_cast<unsigned>(clamp_m1(cvt_i32(fy), c.Hm1) + 1), c.pitch2, ix2);
-            top = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
-            bot = __builtin_amdgcn_raw_buffer_load_b32(rs, off, c.pitch2, 0);
-        }
-        t.top.x = __builtin_bit_cast(float, top);
-        t.bot.x = __builtin_bit_cast(float, bot);
-        return t;
-    }
     const unsigned ix4 = (static_cast<unsigned>(clamp_m1(cvt_i32(fx), c.Wm1)) << 2) + 4u;
     if (Y_IN_RANGE) {
         const unsigned off = mad_u24(static_cast<unsigned>(cvt_i32(fy)), c.pitch4, ix4);
@@ -522,13 +493,6 @@ __device__ __forceinline__ Tap fetch_tap(__amdgpu_buffer_rsrc_t rs, Cam& c, floa
     return t;
 }
 
-// binary16 row pair v = (lo, hi): hi - lo rounded once to binary32 (v_fma_mix_f32 hi * 1 + (-lo)),
-// the same bits as the fp32 subtraction of the two converted texels (conversion is exact)
-__device__ __forceinline__ float f16_pair_diff(unsigned v) {
-    float r;
-    asm("v_fma_mix_f32 %0, %1, 1.0, -%1 op_sel:[1,0,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(v));
-    return r;
-}
 // fmaf(a, d, (float)lo(v)) in one v_fma_mix_f32
 __device__ __forceinline__ float f16_fma_lo(float a, float d, unsigned v) {
     float r;
@@ -556,18 +520,12 @@ __device__ __forceinline__ float f16_fma_hi(float a, float d, unsigned v) {
 
 template <int TEX = 0>
 __device__ __forceinline__ float lerp_tap(const Tap& t) {
-    if (TEX == 1 && ACMMP_TEX_PAIRS) {
+    if (TEX == 1) {
         // (the words stay in the load's own vector type: a round trip through f32x2 lanes was folded
         // into one lane by this compiler)
         const unsigned w0 = t.pw[0], w1 = t.pw[1];
         const float r0 = f16_fma_lo(t.a, f16_lo_diff(w1, w0), w0);
         const float r1 = f16_fma_hi(t.a, f16_hi_diff(w1, w0), w0);
-        return fmaf(t.b, r1 - r0, r0);
-    }
-    if (TEX == 1) {
-        const unsigned top = __builtin_bit_cast(unsigned, t.top.x), bot = __builtin_bit_cast(unsigned, t.bot.x);
-        const float r0 = f16_fma_lo(t.a, f16_pair_diff(top), top);
-        const float r1 = f16_fma_lo(t.a, f16_pair_diff(bot), bot);
         return fmaf(t.b, r1 - r0, r0);
     }
     const float r0 = fmaf(t.a, t.top.y - t.top.x, t.top.x);
@@ -580,39 +538,23 @@ template <int MODEL>
 __device__ __forceinline__ float4 patch_sample(const KParams& kp, int px, int py, int s, int i, int j, float center,
                                                float& r) {
     const DevCam& rc = kp.cams[0];
-    r = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px + i, py + j);
+    r = texel_padded(rc.img_base, rc.img_pitch, rc.W, rc.H, px + i, py + j);
     const float sp = kp.spatial[(MODEL == kSphere ? static_cast<long long>(py) * kp.S : 0) + s];
     const float w = det_exp(sp - fabsf(r - center) / kp.color_den);
     const float4 d = ray_at<MODEL>(kp, px + i, py + j);
     return make_float4(d.x, d.y, d.z, w);
 }
 
-// Stage sample s of pixel (px, py) into its LDS slot.
+// SPHERE's hypothesis- and view-independent weight sums of an unstaged patch (the staged layouts
+// form them in coop_patch_nb / coop_patch_sep, in the same order).
 template <int MODEL>
-__device__ __forceinline__ void stage_sample(const KParams& kp, int px, int py, int s, float center, float4* rw,
-                                             float* rr) {
-    const int i = -kp.R + (s / kp.nside) * kp.inc, j = -kp.R + (s % kp.nside) * kp.inc;
-    float r;
-    *rw = patch_sample<MODEL>(kp, px, py, s, i, j, center, r);
-    *rr = r;
-}
-
-template <int MODEL>
-__device__ __forceinline__ void patch_sums(const KParams& kp, Patch& pt, int px = 0, int py = 0) {
+__device__ __forceinline__ void patch_sums(const KParams& kp, Patch& pt, int px, int py) {
     pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f;
     if (MODEL == kSphere) {
         for (int s = 0; s < kp.S; ++s) {
-            float w, r;
-            if (pt.rw) {
-                w = pt.rw[s * pt.stride].w;
-                r = pt.rr[s * pt.stride];
-            } else if (pt.wr) {
-                w = pt.wr[s * pt.stride].x;
-                r = pt.wr[s * pt.stride].y;
-            } else {
-                w = patch_sample<MODEL>(kp, px, py, s, -kp.R + (s / kp.nside) * kp.inc,
-                                        -kp.R + (s % kp.nside) * kp.inc, pt.center, r).w;
-            }
+            float r;
+            const float w = patch_sample<MODEL>(kp, px, py, s, -kp.R + (s / kp.nside) * kp.inc,
+                                                -kp.R + (s % kp.nside) * kp.inc, pt.center, r).w;
             pt.sbw += w;
             pt.sref = fmaf(w, r, pt.sref);
             pt.srr = fmaf(w * r, r, pt.srr);
@@ -627,25 +569,17 @@ __device__ __forceinline__ Patch make_patch(const KParams& kp, int px, int py) {
     const DevCam& rc = kp.cams[0];
     Patch pt;
     pt.rw = nullptr; pt.rr = nullptr; pt.wr = nullptr; pt.row = pt.col = nullptr; pt.stride = 0;
-    pt.center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
+    pt.center = texel_padded(rc.img_base, rc.img_pitch, rc.W, rc.H, px, py);
     patch_sums<MODEL>(kp, pt, px, py);
     return pt;
 }
 
-// STAGED: 0 = samples recomputed here, 1 = (ray, w) + texel staged in LDS, 2 = (w, texel) staged
-// and the ray re-read from the ray tables (less LDS per pixel, more blocks per CU), 3 = the
-// k_eval_nb layout of coop_patch_nb.
-#ifndef ACMMP_PIPEG
-#define ACMMP_PIPEG 1                       // views per texel-fetch group when the caller does not pipeline
-#endif
-constexpr int kPipeG = ACMMP_PIPEG;
-#ifndef ACMMP_PIPEG16
-#define ACMMP_PIPEG16 ACMMP_PIPEG            // the same for the binary16 fetches (half the tap registers)
-#endif
-constexpr int kPipeG16 = ACMMP_PIPEG16;
-#ifndef ACMMP_RC_CONST_PIPE
-#define ACMMP_RC_CONST_PIPE 0               // 1: PIPE callers (k_eval_ref) also read the reference camera per sample (A/B r01_v27: -3%)
-#endif
+// STAGED: 0 = samples recomputed here, 3 = the k_eval_nb layout of coop_patch_nb, 4 = the separable
+// SPHERE layout of coop_patch_sep.  PIPE: every view's texels of a sample in flight before the first
+// is used (~6 VGPRs per view); otherwise each view's sample is consumed as soon as it arrives
+// (pipelined fetch groups of 2 and 4 views measured neutral to -2%, r01_v29).  PIPE callers keep the
+// reference camera in registers across the loop (read per sample through the constant address space
+// instead: -3%, r01_v27).
 
 template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM = 0, bool FULL = false>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
@@ -653,20 +587,14 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     // FULL: every view of the chunk present (compile-time); otherwise a wave-uniform count, kept in an
     // SGPR so the per-view guards are scalar branches (without it they were lane masks round-tripped
     // through a VGPR: two VALU per view-sample)
-#ifndef ACMMP_NV_UNIFORM
-#define ACMMP_NV_UNIFORM 1
-#endif
-    const int nv = FULL ? VB : (ACMMP_NV_UNIFORM ? uniform_int(nv_rt) : nv_rt);
+    const int nv = FULL ? VB : uniform_int(nv_rt);
     // per-view guard inside the sample loop: `v < nv` hoisted out of the loop is an i1 live across it,
     // which the backend keeps as a lane mask and re-tests through a VGPR (v_cndmask + v_cmp per
     // view-sample); re-reading nv into an SGPR at the use keeps the test a scalar compare.  Applied to
-    // fast-mode SPHERE k_eval_nb-layout chunks (ACMMP_NV_SCALAR_GUARD 2): k_eval_nb -1.5..-2% there,
+    // fast-mode SPHERE k_eval_nb-layout chunks: k_eval_nb -1.5..-2% there,
     // while the pinhole refinement (+2.7%), k_select (+3%) and the exact-mode k_eval_nb (+0.7%) lose
     // (r02 A/B profiles/r02_nv_guard_ab.txt)
-#ifndef ACMMP_NV_SCALAR_GUARD
-#define ACMMP_NV_SCALAR_GUARD 2
-#endif
-    constexpr bool kScalarGuard = ACMMP_NV_SCALAR_GUARD == 1 || (ACMMP_NV_SCALAR_GUARD == 2 && MODEL == kSphere && STAGED == 3 && FM);
+    constexpr bool kScalarGuard = MODEL == kSphere && STAGED == 3 && FM;
     auto has = [&](int v) -> bool {
         if (FULL) return true;
         if constexpr (kScalarGuard) {
@@ -685,7 +613,10 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
         return;
     }
     const DevCam& rc = kp.cams[0];
-    float sbw[VB], sref[VB], srr[VB], ssrc[VB], sss[VB], srs[VB];
+    // (sum w s, sum w r s) and pinhole's (sum w r, sum w r r) per view as packed pairs: one v_pk_fma_f32
+    // per view-sample for each pair (the same fma per sum as separate registers, so the same bits)
+    float sbw[VB], sss[VB];
+    f32x2 ssrs[VB], srrr[VB];
     bool cval[VB];
     int cv[VB];
 #pragma unroll
@@ -700,8 +631,10 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                           : world_point_ray<MODEL>(rc, px, py, depth_from_plane(ph, dc), dc);
 #pragma unroll
     for (int v = 0; v < VB; ++v) {
-        sbw[v] = pt.sbw; sref[v] = pt.sref; srr[v] = pt.srr;
-        ssrc[v] = 0.f; sss[v] = 0.f; srs[v] = 0.f;
+        sbw[v] = pt.sbw;
+        srrr[v] = (f32x2){pt.sref, pt.srr};
+        sss[v] = 0.f;
+        ssrs[v] = splat2(0.f);
         cval[v] = true;
         if (MODEL == kPinhole && v < nv) {
             float ox, oy, od;
@@ -710,16 +643,11 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             cval[v] = !(ox < 0.0f || ox >= PCV(v).Wf || oy < 0.0f || oy >= PCV(v).Hf);
         }
     }
-    // ACMMP_FT_VGPR: fast-mode SPHERE k_eval_nb chunks hold each view's Ft in VGPRs across the loop
-#ifndef ACMMP_FT_VGPR
-#define ACMMP_FT_VGPR 1                     // k_eval_nb -1.3..-1.7%, metric +1% (profiles/r02_ft_vgpr_ab.txt)
-#endif
-    constexpr bool kFtV = ACMMP_FT_VGPR && FM && MODEL == kSphere && STAGED == 3;
-#ifndef ACMMP_CC_VGPR
-#define ACMMP_CC_VGPR 0                     // the same for (cx, cy): 74 VGPRs / 6 waves, not yet measured
-#endif
-    constexpr bool kCcV = kFtV && ACMMP_CC_VGPR;
-    float ftv[VB][3], ccv[VB][2];
+    // fast-mode SPHERE k_eval_nb chunks hold each view's Ft in VGPRs across the loop (a VOP3 fma reads
+    // one SGPR, so a translation in SGPRs costs a move per view-sample): k_eval_nb -1.3..-1.7%, metric +1%
+    // (profiles/r02_ft_vgpr_ab.txt)
+    constexpr bool kFtV = FM && MODEL == kSphere && STAGED == 3;
+    float ftv[VB][3];
 #pragma unroll
     for (int v = 0; v < VB; ++v) {
 #pragma unroll
@@ -727,14 +655,19 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             ftv[v][k] = 0.f;
             if (kFtV) asm volatile("v_mov_b32 %0, %1" : "=v"(ftv[v][k]) : "s"(PCV(v).Ft[k]));
         }
-        ccv[v][0] = ccv[v][1] = 0.f;
-        if (kCcV) {
-            asm volatile("v_mov_b32 %0, %1" : "=v"(ccv[v][0]) : "s"(PCV(v).cx));
-            asm volatile("v_mov_b32 %0, %1" : "=v"(ccv[v][1]) : "s"(PCV(v).cy));
-        }
     }
     const int R = kp.R, inc = kp.inc;
-    constexpr int G = PIPE ? VB : (TEX == 1 ? kPipeG16 : kPipeG);
+    constexpr int G = PIPE ? VB : 1;
+    // PF (fast-mode SPHERE k_eval_nb chunks): the texels of sample s are consumed while sample s + 1's
+    // loads are in flight -- each wave keeps two samples' gathers outstanding, so the gather latency
+    // hides behind the next sample's projection instead of stalling the wave (same accumulation order)
+    constexpr bool PF = PIPE && FM && MODEL == kSphere && STAGED == 3;
+    Tap ptap[VB];
+    float pw = 0.f, pr = 0.f;
+    f32x2 pwwr = splat2(0.f);
+    bool pok[VB];
+#pragma unroll
+    for (int v = 0; v < VB; ++v) pok[v] = false;
     int s = 0, ii = 0;
     for (int i = -R; i <= R; i += inc, ++ii) {
         int jj = 0;                                      // s % nside without a division per sample
@@ -747,23 +680,15 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 const float2 q = pt.wr[s];
                 rw = make_float4(rs.y * cs.x, -rs.x, rs.y * cs.y, q.x);
                 r = q.y;
-            } else if (STAGED == 1) {
-                rw = pt.rw[s * pt.stride];
-                r = pt.rr[s * pt.stride];
             } else if (STAGED == 3) {                    // coop_patch_nb layout
-                const float4 q = pt.rw[s];
+                const float4 q = pt.rw[s * pt.stride];
                 if (MODEL == kSphere) {
-                    rw = make_float4(q.x, pt.rr[jj], q.y, q.z);
+                    rw = make_float4(q.x, pt.rr[jj * pt.stride], q.y, q.z);
                     r = q.w;
                 } else {
                     rw = q;
-                    r = pt.rr[s];
+                    r = pt.rr[s * pt.stride];
                 }
-            } else if (STAGED == 2) {
-                const float2 q = pt.wr[s * pt.stride];
-                rw = ray_at<MODEL>(kp, px + i, py + j);
-                rw.w = q.x;
-                r = q.y;
             } else {
                 rw = patch_sample<MODEL>(kp, px, py, s, i, j, pt.center, r);
             }
@@ -774,42 +699,37 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             const float dep = FM ? depth_from_plane_fast(ph, rw) : depth_from_plane(ph, rw);
             if (FM)
                 P = cam_point_fast<MODEL>(ccams[0], px + i, py + j, dep, rw);
-            else if (!PIPE || ACMMP_RC_CONST_PIPE)
+            else if (!PIPE)
                 P = world_point_ray<MODEL>(ccams[0], px + i, py + j, dep, rw);
             else
                 P = world_point_ray<MODEL>(rc, px + i, py + j, dep, rw);
             const float wr = w * r;
+            const f32x2 wwr = (f32x2){w, wr};
             Tap tap[VB];
             bool ok[VB];
-            // ACMMP_ACC_ALL: with scalar guards, accumulate every view of the chunk without a guard (views
-            // past nv accumulate view 0's texel into sums nobody reads), so the accumulation is one block
-#ifndef ACMMP_ACC_ALL
-#define ACMMP_ACC_ALL 0                     // 1: k_eval_nb +3.5..4.5% (profiles/r02_acc_all_ab.txt)
-#endif
-            constexpr bool kAccAll = ACMMP_ACC_ALL && kScalarGuard && G > 1;
-            // accumulate view v's sample (ACMMP.cu:488-498)
-#define ACMMP_ACCUMULATE(v)                                                  \
+            // accumulate view v's sample (ACMMP.cu:488-498): texel tap T of a sample with weight W_,
+            // (w, w r) = WWR_ and reference texel R_
+#define ACMMP_ACCUMULATE_T(v, T, W_, WWR_, R_, OK_)                          \
             do {                                                             \
-                const float sp = lerp_tap<TEX>(tap[v]);                      \
-                if (MODEL == kSphere ? (kAccAll || has(v)) : ok[v]) {       \
+                const float sp = lerp_tap<TEX>(T);                           \
+                if (MODEL == kSphere ? has(v) : (OK_)) {                     \
                     if (MODEL == kPinhole) {                                 \
-                        sbw[v] += w;                                         \
-                        sref[v] = fmaf(w, r, sref[v]);                       \
-                        srr[v] = fmaf(wr, r, srr[v]);                        \
+                        sbw[v] += (W_);                                      \
+                        srrr[v] = pk_fma(WWR_, splat2(R_), srrr[v]);         \
                     }                                                        \
-                    ssrc[v] = fmaf(w, sp, ssrc[v]);                          \
-                    const float ws = w * sp;                                 \
+                    ssrs[v] = pk_fma(WWR_, splat2(sp), ssrs[v]);             \
+                    const float ws = (W_) * sp;                              \
                     sss[v] = fmaf(ws, sp, sss[v]);                           \
-                    srs[v] = fmaf(wr, sp, srs[v]);                           \
                 }                                                            \
             } while (0)
+#define ACMMP_ACCUMULATE(v) ACMMP_ACCUMULATE_T(v, tap[v], w, wwr, r, ok[v])
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
                 ok[v] = false;
                 if (has(v)) {
                     ConstCam& c = PCV(v);
                     float sx, sy, sd;
-                    if (FM) project_fast<MODEL>(c, P, sx, sy, kFtV ? ftv[v] : nullptr, kCcV ? ccv[v] : nullptr);
+                    if (FM) project_fast<MODEL>(c, P, sx, sy, kFtV ? ftv[v] : nullptr);
                     else project<MODEL>(c, P, sx, sy, sd);
                     ok[v] = true;
                     if (MODEL == kSphere) {
@@ -823,30 +743,46 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(c.img_base), 0, c.img_bytes, 0x00020000);
                     tap[v] = fetch_tap<TEX, MODEL == kSphere>(rs, c, sx, sy);
                     if (G == 1) ACMMP_ACCUMULATE(v);
-                } else if (kAccAll) {
-                    tap[v] = tap[0];
                 }
                 // a full SPHERE chunk has no per-view branches; keep its views' code in view order
                 // (interleaved, their live ranges overlap and the 7-wave register budget spills)
-                if (FULL && MODEL == kSphere && ACMMP_VIEW_BARRIER) __builtin_amdgcn_sched_barrier(0);
+                if (FULL && MODEL == kSphere) __builtin_amdgcn_sched_barrier(0);
                 // G > 1: views are consumed in groups of G, a group's texels all in flight before the
                 // first is used (PIPE: the whole chunk; ~6 VGPRs per view in flight)
-                if (G > 1 && ((v + 1) % G == 0 || v == VB - 1)) {
+                if (!PF && G > 1 && ((v + 1) % G == 0 || v == VB - 1)) {
 #pragma unroll
                     for (int u = v - (v % G); u <= v; ++u)
-                        if (kAccAll || has(u)) ACMMP_ACCUMULATE(u);
+                        if (has(u)) ACMMP_ACCUMULATE(u);
                 }
             }
-#undef ACMMP_ACCUMULATE
+            if constexpr (PF) {
+                if (s > 0) {
+#pragma unroll
+                    for (int u = 0; u < VB; ++u)
+                        if (has(u)) ACMMP_ACCUMULATE_T(u, ptap[u], pw, pwwr, pr, pok[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < VB; ++u) { ptap[u] = tap[u]; pok[u] = ok[u]; }
+                pw = w; pr = r; pwwr = wwr;
+            }
         }
     }
+    if constexpr (PF) {
+        if (s > 0) {
+#pragma unroll
+            for (int u = 0; u < VB; ++u)
+                if (has(u)) ACMMP_ACCUMULATE_T(u, ptap[u], pw, pwwr, pr, pok[u]);
+        }
+    }
+#undef ACMMP_ACCUMULATE
+#undef ACMMP_ACCUMULATE_T
 #pragma unroll
     for (int v = 0; v < VB; ++v) {
         float out = 2.0f;
         if (cval[v] && !(sbw[v] < 1e-6f)) {
             const float inv = 1.0f / sbw[v];
-            const float m_ref = sref[v] * inv, m_src = ssrc[v] * inv;
-            const float e_rr = srr[v] * inv, e_ss = sss[v] * inv, e_rs = srs[v] * inv;
+            const float m_ref = srrr[v].x * inv, m_src = ssrs[v].x * inv;
+            const float e_rr = srrr[v].y * inv, e_ss = sss[v] * inv, e_rs = ssrs[v].y * inv;
             const float var_ref = fmaf(-m_ref, m_ref, e_rr);
             const float var_src = fmaf(-m_src, m_src, e_ss);
             if (!(var_ref < 1e-5f || var_src < 1e-5f)) {
@@ -966,9 +902,7 @@ __device__ __forceinline__ void for_all_views_t(const KParams& kp, int px, int p
         }
         if (nv == 0) break;
         float cost[VB];
-        constexpr bool kFullSph = ACMMP_FULL_CHUNK_SPH == 1 || (ACMMP_FULL_CHUNK_SPH == 2 && VB <= 2) ||
-                                  (ACMMP_FULL_CHUNK_SPH == 3 && VB <= 2 && STAGED == 3);
-        if ((MODEL == kSphere ? kFullSph : ACMMP_FULL_CHUNK_PIN) && VB > 1 && nv == VB)
+        if ((MODEL == kSphere ? VB <= 2 : true) && VB > 1 && nv == VB)
             ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM, true>(kp, px, py, pt, ph, vlist, nv, cost);
         else
             ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM>(kp, px, py, pt, ph, vlist, nv, cost);
@@ -1017,59 +951,28 @@ __device__ __forceinline__ float vw_get(const uint32_t (&vwp)[4], int v) {
 // XCD-aware block order (k_init).  Blocks are dealt round-robin over the 8 XCDs (b and b + 8 share
 // one L2, MI355X_MICROARCH.md "Workgroup dispatch"); launch order gives every XCD every 8th tile of
 // the same rows, so each L2 caches the source-image footprint of all rows in flight.  Instead XCD
-// (b % 8) walks strips x, x + 8, x + 16, ... of ACMMP_XCD_STRIP consecutive logical blocks: its
+// (b % 8) walks strips x, x + 8, x + 16, ... of kXcdStrip consecutive logical blocks: its
 // resident blocks cover 1/8 of the rows in flight, and the strips interleave finely enough that every
 // XCD gets the same mix of short-circuited and evaluated rows.  The grid is padded to whole strips
 // per XCD (xcd_grid); surplus blocks find no pixel.  Measured (r01_v23): k_init -10% at 3200x1600
 // V=15 and -16% at 1600x1200 pinhole V=10, neutral at the metric; the same order made k_eval_nb /
-// k_eval_ref 4-9% SLOWER (their lanes of one pixel already share a footprint), so they keep launch order.
-#ifndef ACMMP_XCD_STRIP
-#define ACMMP_XCD_STRIP 256
-#endif
+// k_eval_ref 2-9% SLOWER (their lanes of one pixel already share a footprint; r01_v23,
+// r02_eval_xcd_strip_ab.txt), so they keep launch order.
+constexpr unsigned kXcdStrip = 256;
 __device__ __forceinline__ long long xcd_block(unsigned b) {
-    if (ACMMP_XCD_STRIP == 0) return b;
     const unsigned x = b & 7u, k = b >> 3;
-    const unsigned j = k / ACMMP_XCD_STRIP, r = k - j * ACMMP_XCD_STRIP;
-    return (static_cast<long long>(j) * 8 + x) * ACMMP_XCD_STRIP + r;
+    const unsigned j = k / kXcdStrip, r = k - j * kXcdStrip;
+    return (static_cast<long long>(j) * 8 + x) * kXcdStrip + r;
 }
 
 static inline unsigned xcd_grid(long long nblocks) {
-    if (ACMMP_XCD_STRIP == 0) return static_cast<unsigned>(nblocks);
-    const long long strips = (nblocks + ACMMP_XCD_STRIP - 1) / ACMMP_XCD_STRIP;
-    return static_cast<unsigned>((strips + 7) / 8 * 8 * ACMMP_XCD_STRIP);
-}
-
-// The same remap with its own strip length for the evaluation kernels (0 = launch order).
-#ifndef ACMMP_EVAL_XCD_STRIP
-#define ACMMP_EVAL_XCD_STRIP 0
-#endif
-__device__ __forceinline__ long long eval_block(unsigned b) {
-    if (ACMMP_EVAL_XCD_STRIP == 0) return b;
-    const unsigned x = b & 7u, k = b >> 3;
-    const unsigned j = k / ACMMP_EVAL_XCD_STRIP, r = k - j * ACMMP_EVAL_XCD_STRIP;
-    return (static_cast<long long>(j) * 8 + x) * ACMMP_EVAL_XCD_STRIP + r;
-}
-static inline unsigned eval_grid(long long nblocks) {
-    if (ACMMP_EVAL_XCD_STRIP == 0) return static_cast<unsigned>(nblocks);
-    const long long strips = (nblocks + ACMMP_EVAL_XCD_STRIP - 1) / ACMMP_EVAL_XCD_STRIP;
-    return static_cast<unsigned>((strips + 7) / 8 * 8 * ACMMP_EVAL_XCD_STRIP);
+    const long long strips = (nblocks + kXcdStrip - 1) / kXcdStrip;
+    return static_cast<unsigned>((strips + 7) / 8 * 8 * kXcdStrip);
 }
 
 // ------------------------------------------------------------------ kernels: setup
 
 #if ACMMP_IN_TU(0)
-__global__ void k_to_f16(const float* __restrict__ src, long long n, uint16_t* __restrict__ dst,
-                         int* __restrict__ inexact) {
-    const long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const float x = src[i];
-    const _Float16 h = static_cast<_Float16>(x);
-    const float back = static_cast<float>(h);
-    // exact, finite, and zero or normal binary16 (no subnormal inputs to v_fma_mix_f32)
-    if (!(back == x) || (x != 0.0f && !(fabsf(x) >= 6.103515625e-05f)) || fabsf(x) > 65504.0f) atomicOr(inexact, 1);
-    dst[i] = __builtin_bit_cast(uint16_t, h);
-}
-
 // Row-pair binary16 layout of one padded view: word (X, Y) = (h(I[Y][X]), h(I[Y+1][X])) for Y in [0, H].
 __global__ void k_to_f16_pairs(const float* __restrict__ src, int W2, int rows, uint32_t* __restrict__ dst,
                                int* __restrict__ inexact) {
@@ -1212,10 +1115,7 @@ enum InitBranch { kInitRandom = 0, kInitPlanar = 1, kInitUpsample = 2, kInitReus
 // and rays, and with the fast-math projection the wider chunk wins (r02 A/B profiles/r02_init_vb_ab.txt:
 // 2 -> 4 views: 0.95 -> 0.92 ms at the metric, 2.46 -> 2.15 ms at C2, 8.27 -> 6.97 ms at C3; round 1,
 // exact mode only: 1 view 1.55, 2 views 1.36, 4 views 1.41 ms at the metric).
-#ifndef ACMMP_INIT_VB
-#define ACMMP_INIT_VB 4
-#endif
-[[maybe_unused]] constexpr int kInitVB = ACMMP_INIT_VB;
+[[maybe_unused]] constexpr int kInitVB = 4;
 
 template <int MODEL, int VB, int BR, int VMAXB, int TF>
 __global__ __launch_bounds__(256) void k_init(const KParams kp) {
@@ -1265,7 +1165,7 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
                                              static_cast<float>(kp.H) / kp.scaled_rows));
         const int nn = (Imagescale * Imagescale + 1) / 2;
         const float o_y = static_cast<float>(y) * scale, o_x = static_cast<float>(x) * scale;
-        const float* ref = kp.img + rc.img_off;
+        const float* ref = rc.img_base;
         const float refPix = texel_padded(ref, rc.img_pitch, rc.W, rc.H, x, y);
         float nf = 0.0f;
         float nx = 0.f, ny = 0.f, nz = 0.f;
@@ -1438,46 +1338,16 @@ __device__ __forceinline__ bool colour_pixel(const KParams& kp, int colour, long
     return py < kp.row_hi && px < kp.W;
 }
 
-// Cooperative staging of the block's pixels: lane `h` of the `nh` lanes of pixel slot `lp`
-// stages samples h, h+nh, ...; the first lane of each pixel then forms the SPHERE sums.
-template <int MODEL>
-__device__ __forceinline__ Patch coop_patch(const KParams& kp, bool valid, int px, int py, int lp, int h, int nh,
-                                            float4* lrw, float* lrr) {
-    float4* rw = lrw + lp * kp.S;
-    float* rr = lrr + lp * kp.S;
-    if (valid) {
-        const DevCam& rc = kp.cams[0];
-        const float center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
-        for (int s = h; s < kp.S; s += nh) stage_sample<MODEL>(kp, px, py, s, center, rw + s, rr + s);
-    }
-    __syncthreads();
-    Patch pt;
-    pt.rw = rw; pt.rr = rr; pt.wr = nullptr; pt.row = pt.col = nullptr; pt.stride = 1;
-    pt.center = 0.f;
-    // every lane of the pixel sums its SPHERE weights itself (same order, same bits): no LDS slot
-    // and no second barrier, which keeps k_eval_nb's block at 20160 B of LDS (8 blocks per CU)
-    if (valid) patch_sums<MODEL>(kp, pt);
-    else { pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f; }
-    return pt;
-}
-
 // k_eval_nb staging, 16 B per sample + 4 B per patch row: SPHERE stores (ray.x, ray.z, w, texel)
 // per sample and ray.y = -sin(lat) once per patch row (it depends on the row only); PINHOLE stores
 // (ray, w) per sample and the texels after them.  32 pixels x 36 samples = 19.2 KB per block for
 // SPHERE (8 blocks per CU).
 // views per NCC chunk in the evaluation kernels (more views than this run as several chunks:
 // the per-sample world point is recomputed per chunk, the accumulators stay in registers)
-#ifndef ACMMP_EVAL_VB
-#define ACMMP_EVAL_VB 4
-#endif
-constexpr int kEvalVB = ACMMP_EVAL_VB;
-#ifndef ACMMP_NB_PIPE
-#define ACMMP_NB_PIPE false                 // experiment switch: all views' texels in flight in k_eval_nb
-#endif
-#ifndef ACMMP_NB_PIPE_FAST
-#define ACMMP_NB_PIPE_FAST true             // the same in fast-math mode, whose shorter projection leaves the
-                                            // registers for it (r02 A/B: k_eval_nb 2.19 -> 2.06 ms; exact -4%)
-#endif
+constexpr int kEvalVB = 4;
+// k_eval_nb keeps every view's texels of a sample in flight (PIPE) in fast-math mode only, whose shorter
+// projection leaves the registers for it (r02 A/B: k_eval_nb 2.19 -> 2.06 ms; the exact mode -4%)
+constexpr bool kNbPipeExact = false, kNbPipeFast = true;
 constexpr int kNbLanes = 8;                 // the 8 neighbour directions (the current plane's costs are cached)
 constexpr int kNbPix = 32;                  // pixels per 256-lane block
 
@@ -1486,36 +1356,38 @@ static inline size_t nb_lds_bytes(int model, int S, int nside, int npix = kNbPix
                             : (sizeof(float4) + sizeof(float)) * S * npix;
 }
 
+// Sample-major: entry s of pixel slot lp sits at [s * NPIX + lp], so lanes of consecutive pixel slots
+// reading one sample read consecutive 16-byte words (no bank conflicts).
 template <int MODEL, int NPIX = kNbPix, int NLANES = kNbLanes>
 __device__ __forceinline__ Patch coop_patch_nb(const KParams& kp, bool valid, int px, int py, int lp, int h,
                                                float4* lds) {
-    float4* rw = lds + lp * kp.S;
+    float4* rw = lds + lp;
     float* tail = reinterpret_cast<float*>(lds + NPIX * kp.S);
-    float* rr = tail + lp * (MODEL == kSphere ? kp.nside : kp.S);
+    float* rr = tail + lp;
     if (valid) {
         const DevCam& rc = kp.cams[0];
-        const float center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
+        const float center = texel_padded(rc.img_base, rc.img_pitch, rc.W, rc.H, px, py);
         for (int s = h; s < kp.S; s += NLANES) {
             const int i = -kp.R + (s / kp.nside) * kp.inc, j = -kp.R + (s % kp.nside) * kp.inc;
             float r;
             const float4 q = patch_sample<MODEL>(kp, px, py, s, i, j, center, r);
             if (MODEL == kSphere) {
-                rw[s] = make_float4(q.x, q.z, q.w, r);
-                if (s < kp.nside) rr[s] = q.y;          // samples 0..nside-1 cover every patch row j
+                rw[s * NPIX] = make_float4(q.x, q.z, q.w, r);
+                if (s < kp.nside) rr[s * NPIX] = q.y;   // samples 0..nside-1 cover every patch row j
             } else {
-                rw[s] = q;
-                rr[s] = r;
+                rw[s * NPIX] = q;
+                rr[s * NPIX] = r;
             }
         }
     }
     __syncthreads();
     Patch pt;
-    pt.rw = rw; pt.rr = rr; pt.wr = nullptr; pt.row = pt.col = nullptr; pt.stride = 1;
+    pt.rw = rw; pt.rr = rr; pt.wr = nullptr; pt.row = pt.col = nullptr; pt.stride = NPIX;
     pt.center = 0.f;
     pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f;
     if (MODEL == kSphere && valid) {
         for (int s = 0; s < kp.S; ++s) {                // patch_sums order (ACMMP.cu:482-486)
-            const float w = rw[s].z, r = rw[s].w;
+            const float w = rw[s * NPIX].z, r = rw[s * NPIX].w;
             pt.sbw += w;
             pt.sref = fmaf(w, r, pt.sref);
             pt.srr = fmaf(w * r, r, pt.srr);
@@ -1539,7 +1411,7 @@ __device__ __forceinline__ Patch coop_patch_sep(const KParams& kp, bool valid, i
     float2* col = row + kp.nside;
     if (valid) {
         const DevCam& rc = kp.cams[0];
-        const float center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
+        const float center = texel_padded(rc.img_base, rc.img_pitch, rc.W, rc.H, px, py);
         for (int s = h; s < kp.S; s += NLANES) {
             const int i = -kp.R + (s / kp.nside) * kp.inc, j = -kp.R + (s % kp.nside) * kp.inc;
             float r;
@@ -1567,60 +1439,21 @@ __device__ __forceinline__ Patch coop_patch_sep(const KParams& kp, bool valid, i
     return pt;
 }
 
-// Lite staging: only (w, texel) per sample in LDS (8 B instead of 20 B).
-template <int MODEL>
-__device__ __forceinline__ Patch coop_patch_lite(const KParams& kp, bool valid, int px, int py, int lp, int h,
-                                                 int nh, float2* lwr) {
-    float2* wr = lwr + lp * kp.S;
-    if (valid) {
-        const DevCam& rc = kp.cams[0];
-        const float center = texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py);
-        for (int s = h; s < kp.S; s += nh) {
-            const int i = -kp.R + (s / kp.nside) * kp.inc, j = -kp.R + (s % kp.nside) * kp.inc;
-            float r;
-            const float w = patch_sample<MODEL>(kp, px, py, s, i, j, center, r).w;
-            wr[s] = make_float2(w, r);
-        }
-    }
-    __syncthreads();
-    Patch pt;
-    pt.rw = nullptr; pt.rr = nullptr; pt.wr = wr; pt.row = pt.col = nullptr; pt.stride = 1;
-    pt.center = 0.f;
-    if (valid) patch_sums<MODEL>(kp, pt);
-    else { pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f; }
-    return pt;
-}
-
-#ifndef ACMMP_REF_PIPE
-#define ACMMP_REF_PIPE true                 // k_eval_ref: every view's texels in flight (two-phase fetch)
-#endif
-#ifndef ACMMP_REF_WAVES
-#define ACMMP_REF_WAVES 1                   // k_eval_ref: minimum waves per SIMD the register budget must allow
-#endif
-#ifndef ACMMP_REF_WAVES_SPH
-#define ACMMP_REF_WAVES_SPH ACMMP_REF_WAVES // the same for the SPHERE non-geom instance (80 VGPRs at 6 waves, no spills)
-#endif
-#ifndef ACMMP_REF_LITE
-#define ACMMP_REF_LITE 0                    // k_eval_ref: 1 = (w, texel) staging, rays re-read from the tables
-#endif
-#ifndef ACMMP_REF_SEP
-#define ACMMP_REF_SEP 1                     // k_eval_ref (SPHERE, V <= 4): separable staging, 8 blocks per CU instead of 5
-#endif                                      // (r02 A/B: metric +0.8%, exact +0.9%; V = 15 -0.5%, so not there)
-#ifndef ACMMP_REF_VBA_WIDE
-#define ACMMP_REF_VBA_WIDE 1                // SPHERE: 2-view chunks for V > 4 launches too (r02 A/B: V = 15 +1.4%,
-#endif                                      // k_eval_ref -5%; pinhole V = 10 -4%, so SPHERE only)
-#ifndef ACMMP_REF_VBA
-#define ACMMP_REF_VBA 2                     // k_eval_ref / tail: 2-view NCC chunks where launches have 4-view ones (r01_v40 A/B +1.7%)
-#endif
+// k_eval_ref / tail: every view's texels of a sample in flight (two-phase fetch); no register budget
+// (SPHERE's non-geom instance: 80 VGPRs at 6 waves, no spills).  SPHERE launches with V <= 4 stage the
+// patch separably (coop_patch_sep: 8 blocks per CU instead of 5; r02 A/B: metric +0.8%, exact +0.9%,
+// V = 15 -0.5%, so not there; (w, texel)-only staging with the rays re-read from the tables measured
+// no better, r01_v40).  NCC chunks of 2 views where the launch has 4-view ones (r01_v40 A/B +1.7%),
+// and for SPHERE launches with V > 4 too (r02 A/B: V = 15 +1.4%; pinhole V = 10 -4%, so not pinhole).
+constexpr bool kRefPipe = true;
+template <int MODEL, int VB>
+constexpr int ref_vb() { return (VB == 4 || (VB > 4 && MODEL == kSphere)) ? 2 : (VB > kEvalVB ? kEvalVB : VB); }
 constexpr int kRefLanes = 5;                // refinement candidates (ACMMP.cu:870)
 constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 lanes used)
 
 // Adaptive checkerboard sampling of every pixel of the colour, one direction per grid row: the
 // direction is wave-uniform here, where inside k_eval_nb (lane = direction) a wave walks all eight
-// of pick_neighbour's cases one after the other.
-#ifndef ACMMP_PICK_PASS
-#define ACMMP_PICK_PASS 1
-#endif
+// of pick_neighbour's cases one after the other (k_eval_nb 2.84 -> 2.60 ms, r01_v38).
 #if ACMMP_IN_TU(0)
 __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour) {
     const long long q = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -1633,29 +1466,21 @@ __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour
 
 #endif  // ACMMP_IN_TU(0)
 
-#ifndef ACMMP_NB_VIEW_CHUNK_DEFAULT
-#define ACMMP_NB_VIEW_CHUNK_DEFAULT 0       // views per k_eval_nb launch (0 = all in one launch)
-#endif
-#ifndef ACMMP_NB_WAVES
-#define ACMMP_NB_WAVES 8                    // k_eval_nb (SPHERE): minimum waves per SIMD the register budget must allow
-#endif
+// k_eval_nb register budgets (minimum waves per SIMD): SPHERE exact 8, SPHERE fast 7 (72 VGPRs, no
+// spills; r02 A/B: 7 waves +0.6% over 8), pinhole none.
 // TEX (binary16 texels) and FM (fast math) are compile-time here, so each of the four variants gets its
 // own register allocation (a runtime branch between them sized every variant for the largest: 23
 // VGPRs spilled at the 64-VGPR budget; r02 A/B profiles/r02_split_nb_ab.txt: fast 388 -> 394, exact
 // 316.6 -> 320 Mpixel-iterations/s)
-#ifndef ACMMP_NB_WAVES_FM
-#define ACMMP_NB_WAVES_FM 7                 // the fast-math instances: 72 VGPRs, no spills (r02 A/B: 7 waves +0.6% over 8)
-#endif
 template <int MODEL, int VB, int TEX, int FM>
-#ifndef ACMMP_NB_WAVES_PIN
-#define ACMMP_NB_WAVES_PIN 1                // pinhole instances: no register budget
-#endif
-__global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_WAVES_FM : ACMMP_NB_WAVES) : ACMMP_NB_WAVES_PIN) void k_eval_nb(
+__global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? 5 : 8) : 1) void k_eval_nb(
     const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
+    // 8 lanes per pixel, one per neighbour direction (a pixel-major map -- a wave = 32 pixels x 2
+    // directions -- measured 3% slower, profiles/r03_ab1_packed_pixelmajor.txt)
     const int lp = t / kNbLanes, h = t - lp * kNbLanes;
-    const long long q = eval_block(blockIdx.x) * kNbPix + lp;
+    const long long q = static_cast<long long>(blockIdx.x) * kNbPix + lp;
     int px = 0, py = 0;
     const bool valid = colour_pixel(kp, colour, q, px, py);
     const Patch pt = coop_patch_nb<MODEL>(kp, valid, px, py, lp, h, lds4);
@@ -1665,27 +1490,20 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_WAVES_FM : A
     if (!valid) return;
     const long long Pc = kp.Pc;
     const long long ci = static_cast<long long>(py) * kp.Wh + (px >> 1);
-#if ACMMP_PICK_PASS
     const int pos = kp.nbpos[h * Pc + ci];                  // k_pick
-#else
-    const int pos = pick_neighbour(kp, h, px, py);
-    kp.nbpos[h * Pc + ci] = pos;
-#endif
     if (pos < 0) return;
     const float4 ph = plane_at(kp, pos);
     const uint32_t all = kp.nb_views;
     float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
-    for_all_views_t<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, FM ? ACMMP_NB_PIPE_FAST : ACMMP_NB_PIPE, TEX, FM>(
+    for_all_views_t<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
         kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
 }
 
 // Joint view selection, aggregation, acceptance and refinement candidates (ACMMP.cu:1146-1311,
 // 797-874).  `iter` selects the view-selection threshold 0.8 exp(-iter^2 / 90) (:1163).
+// k_select: 5 waves per SIMD (96 VGPRs; r01_v24 A/B: 1 -> 5 waves -5%, 6 waves spills)
 template <int MODEL, int VB, bool GEOM>
-#ifndef ACMMP_SEL_WAVES
-#define ACMMP_SEL_WAVES 5                   // k_select: 5 waves per SIMD (96 VGPRs; r01_v24 A/B: 1 -> 5 waves -5%, 6 waves spills)
-#endif
-__global__ __launch_bounds__(256, ACMMP_SEL_WAVES) void k_select(const KParams kp, const int colour, const int iter) {
+__global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int colour, const int iter) {
     const long long q = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
     int px = 0, py = 0;
     if (!colour_pixel(kp, colour, q, px, py)) return;
@@ -1844,9 +1662,6 @@ __global__ __launch_bounds__(256, ACMMP_SEL_WAVES) void k_select(const KParams k
     uint32_t miss = 0u;
     for (int v = 0; v < V; ++v)
         if (vw_get(vwp, v) > 0.0f && cvec[v * Pc] != cvec[v * Pc]) miss |= 1u << v;
-#ifdef ACMMP_EXP_NOFILL
-    miss = 0u;                                              // A/B experiment only (wrong results)
-#endif
     if (miss) {
         const Patch pt = make_patch<MODEL>(kp, px, py);
         for_all_views<MODEL, 1, 0, true>(kp, px, py, pt, cur_plane, wave_or(miss, V), [&](int v, float c) {
@@ -2020,11 +1835,11 @@ __global__ __launch_bounds__(256, ACMMP_SEL_WAVES) void k_select(const KParams k
 
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
 template <int MODEL, int VB, bool GEOM, int TF>
-__global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_SPH : ACMMP_REF_WAVES) void k_eval_ref(const KParams kp, const int colour) {
+__global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
-    const long long q = eval_block(blockIdx.x) * kRefPix + lp;
+    const long long q = static_cast<long long>(blockIdx.x) * kRefPix + lp;
     int px = 0, py = 0;
     bool valid = t < kRefPix * kRefLanes && colour_pixel(kp, colour, q, px, py);
     const long long Pc = kp.Pc;
@@ -2037,21 +1852,16 @@ __global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_
         vw = st.vw;
         weight_norm = st.weight_norm;
     }
-#if ACMMP_REF_LITE
-    constexpr int kStaged = 2;
-    const Patch pt = coop_patch_lite<MODEL>(kp, valid, px, py, lp, h, kRefLanes, reinterpret_cast<float2*>(lds4));
-#else
-    constexpr int kStaged = (MODEL == kSphere && ACMMP_REF_SEP && VB <= 4) ? 4 : 3;
+    constexpr int kStaged = (MODEL == kSphere && VB <= 4) ? 4 : 3;
     Patch pt;
     if constexpr (kStaged == 4) pt = coop_patch_sep<kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
     else pt = coop_patch_nb<MODEL, kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
-#endif
-    constexpr int VBA = ((VB == 4 || (VB > 4 && MODEL == kSphere && ACMMP_REF_VBA_WIDE)) && ACMMP_REF_VBA == 2) ? 2 : (VB > kEvalVB ? kEvalVB : VB);
+    constexpr int VBA = ref_vb<MODEL, VB>();
     if (!valid) return;
     if (kp.ref_split > 0 && h == 0) {                        // the tail's patch, without re-summing it
         const DevCam& rc = kp.cams[0];
         kp.psum[ci] = make_float4(pt.sbw, pt.sref, pt.srr,
-                                  texel_padded(kp.img + rc.img_off, rc.img_pitch, rc.W, rc.H, px, py));
+                                  texel_padded(rc.img_base, rc.img_pitch, rc.W, rc.H, px, py));
     }
     const float4 dc = ray_at<MODEL>(kp, px, py);
     const float4 tp = kp.cand[h * Pc + ci];
@@ -2070,7 +1880,7 @@ __global__ __launch_bounds__(256, (MODEL == kSphere && !GEOM) ? ACMMP_REF_WAVES_
     float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
     for (int v = 0; v < kp.V; ++v)
         if (!((amask >> v) & 1u)) vcost[v * Pc] = __builtin_nanf("");
-    for_all_views_tf<MODEL, VBA, kStaged, ACMMP_REF_PIPE, TF>(kp, px, py, pt, tp, amask, [&](int v, float c) {
+    for_all_views_tf<MODEL, VBA, kStaged, kRefPipe, TF>(kp, px, py, pt, tp, amask, [&](int v, float c) {
         vcost[v * Pc] = c;
         const float w = vw_get(vwp, v);
         if (w > 0.0f) {
@@ -2129,8 +1939,8 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
         pt.sbw = ps.x; pt.sref = ps.y; pt.srr = ps.z; pt.center = ps.w;
         float temp_cost = kp.cand_cost[h * Pc + ci];
         float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
-        constexpr int VBT = ((VB == 4 || (VB > 4 && MODEL == kSphere && ACMMP_REF_VBA_WIDE)) && ACMMP_REF_VBA == 2) ? 2 : (VB > kEvalVB ? kEvalVB : VB);
-        for_all_views_tf<MODEL, VBT, 0, ACMMP_REF_PIPE, TF>(kp, px, py, pt, tp, umask, [&](int v, float c) {
+        constexpr int VBT = ref_vb<MODEL, VB>();
+        for_all_views_tf<MODEL, VBT, 0, kRefPipe, TF>(kp, px, py, pt, tp, umask, [&](int v, float c) {
             vcost[v * Pc] = c;
             const float w = vw_get(vwp, v);
             if (w > 0.0f) {
@@ -2366,19 +2176,12 @@ __global__ void k_debug(const KParams kp, int which, int n, const int* __restric
 static inline int cdiv(long long a, int b) { return static_cast<int>((a + b - 1) / b); }
 
 #if ACMMP_IN_TU(0)
-hipError_t launch_to_f16(const float* src, long long n, uint16_t* dst, int* inexact, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    k_to_f16<<<static_cast<unsigned>((n + 255) / 256), 256, 0, s>>>(src, n, dst, inexact);
-    return hipGetLastError();
-}
-
 hipError_t launch_to_f16_pairs(const float* src, int W, int H, uint32_t* dst, int* inexact, hipStream_t s) {
     const long long n = static_cast<long long>(W + 2) * (H + 1);
     k_to_f16_pairs<<<static_cast<unsigned>((n + 255) / 256), 256, 0, s>>>(src, W + 2, H + 1, dst, inexact);
     return hipGetLastError();
 }
 
-int tex_pairs_layout() { return ACMMP_TEX_PAIRS; }
 
 hipError_t launch_pad_image(const float* src, size_t pitch_floats, int W, int H, float* dst, int dst_pitch,
                             hipStream_t s) {
@@ -2475,8 +2278,8 @@ hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s);
 // launch over all views); read per half-sweep.
 static int nb_view_chunk(const KParams& kp) {
     const char* e = std::getenv("ACMMP_NB_VIEW_CHUNK");
-    int c = e ? std::atoi(e) : ACMMP_NB_VIEW_CHUNK_DEFAULT;
-    if (!e && c == 0) {
+    int c = e ? std::atoi(e) : 0;
+    if (!e) {
         // texel bytes of the sources at the reference's size (row-pair binary16 or fp32: 4 B per texel)
         const double bytes = 4.0 * (kp.W + 2) * (kp.H + 2) * kp.V;
         c = (kp.V > 8 && bytes > 160e6) ? 8 : 0;
@@ -2501,7 +2304,7 @@ hipError_t launch_eval_nb(const KParams& kp0, int colour, hipStream_t s) {
 hipError_t launch_eval_nb_views(const KParams& kp, int colour, hipStream_t s) {
     const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
     const size_t lds_nb = nb_lds_bytes(kp.model, kp.S, kp.nside);
-    const dim3 grd = eval_grid(cdiv(npix, kNbPix));
+    const dim3 grd = static_cast<unsigned>(cdiv(npix, kNbPix));
     if (kp.fast) {
         if (kp.tex16) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 1, 1><<<grd, 256, lds_nb, s>>>(kp, colour)));
         else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 0, 1><<<grd, 256, lds_nb, s>>>(kp, colour)));
@@ -2525,12 +2328,11 @@ hipError_t launch_select(const KParams& kp, int colour, int iter, hipStream_t s)
 #if ACMMP_IN_TU(4)
 hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s) {
     const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
-    const size_t lds_ref = ACMMP_REF_LITE ? sizeof(float2) * kp.S * kRefPix
-                         : (kp.model == kSphere && ACMMP_REF_SEP && pick_vb(kp.V) <= 4) ? sep_lds_bytes(kp.S, kp.nside, kRefPix)
-                                                                 : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
+    const size_t lds_ref = (kp.model == kSphere && pick_vb(kp.V) <= 4) ? sep_lds_bytes(kp.S, kp.nside, kRefPix)
+                                                                       : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
     hipError_t e = hipSuccess;
     if (kp.ref_split > 0 && (e = hipMemsetAsync(kp.surv_count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
-    const dim3 grd_ref = eval_grid(cdiv(npix, kRefPix));
+    const dim3 grd_ref = static_cast<unsigned>(cdiv(npix, kRefPix));
     if (kp.geom) ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, true, TF><<<grd_ref, 256, lds_ref, s>>>(kp, colour))));
     else ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, false, TF><<<grd_ref, 256, lds_ref, s>>>(kp, colour))));
     if (kp.ref_split > 0) {
@@ -2550,7 +2352,7 @@ hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut ou
 #define ACMMP_MARK(i) if (ev && (e = hipEventRecord(ev[i], s)) != hipSuccess) return e
     // k_pick sits outside the four timed buckets (rocprof lists it): the k_eval_nb bucket the bench's
     // roofline prices is that kernel alone
-    if (ACMMP_PICK_PASS) k_pick<<<dim3(cdiv(npix, 256), 8), 256, 0, s>>>(kp, colour);
+    k_pick<<<dim3(cdiv(npix, 256), 8), 256, 0, s>>>(kp, colour);
     ACMMP_MARK(0);
     if ((e = launch_eval_nb(kp, colour, s)) != hipSuccess) return e;
     ACMMP_MARK(1);

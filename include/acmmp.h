@@ -25,7 +25,7 @@ extern "C" {
 
 #define ACMMP_ABI_VERSION 1
 
-/* CameraModel, main.h:184-187 */
+/* CameraModel, main.h:35-38 */
 #define ACMMP_PINHOLE 0
 #define ACMMP_SPHERE 11
 
@@ -77,6 +77,7 @@ typedef enum acmmp_status {
 } acmmp_status;
 
 typedef struct acmmp_ctx acmmp_ctx;
+typedef struct acmmp_image_cache acmmp_image_cache;
 typedef struct acmmp_comm acmmp_comm;
 typedef struct acmmp_fusion acmmp_fusion;
 #define ACMMP_COMM_ID_BYTES 128
@@ -99,8 +100,8 @@ int acmmp_device_count(void);
  * bit-identical to the CPU oracle.  ACMMP_MATH_FAST: what the reference's --use_fast_math build
  * (CMakeLists.txt:42) does to the same arithmetic -- hardware rsq/sqrt/rcp (<= 1 ulp), the
  * translation folded into the rotation, the asin/atan2 polynomials without special-argument paths
- * (DESIGN.md §2.4); results within SURVEY.md §8c's tolerances, not bit-identical.  The environment
- * variable ACMMP_MATH=fast sets the default of new contexts.  No reference counterpart. */
+ * (DESIGN.md §2.4); results within the tolerances of DESIGN.md §2.4, not bit-identical.  Every new
+ * context starts exact; callers choose fast explicitly.  No reference counterpart. */
 enum { ACMMP_MATH_EXACT = 0, ACMMP_MATH_FAST = 1 };
 acmmp_status acmmp_set_math(acmmp_ctx *ctx, int mode);
 int acmmp_get_math(const acmmp_ctx *ctx);
@@ -120,6 +121,24 @@ acmmp_status acmmp_upload_views(acmmp_ctx *ctx, int n, const float *const *image
  * images[i] are device pointers, otherwise as acmmp_upload_views.  No reference counterpart. */
 acmmp_status acmmp_upload_views_device(acmmp_ctx *ctx, int n, const float *const *dev_images,
                                        const size_t *pitch_bytes, const acmmp_camera *cams);
+
+/* Device-side cache of prepared source images (padded fp32 + binary16 copies), shared by the contexts
+ * of one GPU.  The reference re-reads, re-converts and re-uploads every image of every problem
+ * (InuputInitialization ACMMP.cpp:567-643 + CudaSpaceInitialization :685-712); a pipeline that keys its
+ * (view, scale) images prepares each once.  budget_bytes: soft limit (least recently used entries no
+ * current problem uses are freed beyond it), 0 = none.  Destroy after every context that used it. */
+acmmp_status acmmp_image_cache_create(int device, size_t budget_bytes, acmmp_image_cache **out);
+void acmmp_image_cache_destroy(acmmp_image_cache *cache);
+/* out = {hits, misses, bytes held, entries, evictions} */
+acmmp_status acmmp_image_cache_stats(acmmp_image_cache *cache, unsigned long long out[5]);
+
+/* acmmp_upload_views (device_src = 0) / acmmp_upload_views_device (device_src = 1) with a content key
+ * per view: keys[i] != 0 names the exact pixels of images[i] (the caller's promise -- e.g. view id and
+ * scale); a view whose key and size are already in `cache` is not copied or converted again.  keys[i]
+ * = 0 or cache = NULL: prepared privately, as acmmp_upload_views does.  No reference counterpart. */
+acmmp_status acmmp_upload_views_keyed(acmmp_ctx *ctx, acmmp_image_cache *cache, int n, const uint64_t *keys,
+                                      const float *const *images, const size_t *pitch_bytes,
+                                      const acmmp_camera *cams, int device_src);
 
 /* Geometric-consistency depth textures (ACMMP.cpp:653-678, 726-751): n depth maps,
  * depths[i] is h[i] x w[i] row-major (index 0 = reference, as the reference). */

@@ -1,20 +1,32 @@
-"""Fast-math engine mode (acmmp_set_math 'fast') -- tolerance parity, SURVEY.md §8c.
+"""Fast-math engine mode (acmmp_set_math 'fast') -- tolerance parity at BASELINE.json's
+configurations, against the exact mode (bit-identical to the CPU oracle) and a float64 restatement of
+ComputeBilateralNCC (np_reference.py).
 
-The fast mode changes only the NCC's per-sample projection arithmetic (hardware rsq / sqrt / rcp,
-shorter atan polynomial, the translation folded into the rotation), as the reference's own
---use_fast_math build does (CMakeLists.txt:42).  It cannot be bit-identical to the oracle, so it is
-held to tolerances:
+The fast mode changes only the NCC's per-sample projection arithmetic (hardware rsq / sqrt / rcp, the
+latitude and longitude through one packed minimax atan, the source transform in the reference frame),
+as the reference's own --use_fast_math build does to the same code (CMakeLists.txt:42).  It cannot be
+bit-identical, so it is held to the gates DESIGN.md §2.4 states, measured in profiles/r03_fastmath_floor.json
+(scripts/fastmath_floor.py):
 
-  T1  NCC queries: the same {valid, 2.0} classification as the exact mode; the fast mode's distance
-      to a float64 restatement of ComputeBilateralNCC (np_reference.py) no larger than the exact
-      mode's own float32 distance to it, + 1e-4, at the median and the 99th percentile.
-      (|fast - exact| <= 1e-4 holds for >= 99.5% of pinhole queries and <= 1e-3 for all; SPHERE patches, whose
-      bilateral weights leave few effective samples, amplify last-bit differences to ~1e-3 -- the
-      same size as the exact float32 path's own distance to float64.)
-  T2  winners: after RandomInitialization every plane is identical (same RNG draws) and >= 99.5% of
-      costs agree within 1e-3; after one black half-sweep >= 98.5% of pixels hold the same plane.
-  T3  full RunPatchMatch: >= 99% of pixels with finite depths agree within 1%, and accuracy against
-      ground truth within +-0.5 percentage points of the exact mode.
+  T1  NCC queries near the surface.  (a) The {valid, 2.0} classification agrees with the exact mode's as
+      often as the exact mode's agrees with float64's (its thresholds are discontinuities binary32 noise
+      can cross: 99.5% at the metric view), and for >= 99% of queries.
+      (b) Pinhole: |fast - exact| <= 1e-4 for >= 99.5% of valid queries.  SPHERE: the
+      binary32 noise floor of the reference's own arithmetic is far above 1e-4 -- the exact float32
+      path is within 1e-4 of float64 for only ~87% of valid queries at the metric view (few effective
+      samples under the sigma-in-radians weights, E[x^2] - E[x]^2 cancellation) -- so the gate is that
+      fast departs from exact by > 1e-4 no more often than exact departs from float64, + 5 points.
+      (c) No systematic accuracy loss: the fraction of queries where fast is farther from float64 than
+      exact by > 1e-4 is at most the converse fraction + 3 points.
+  T2  After RandomInitialization every plane is identical (same RNG draws) and costs agree within 1e-3
+      for >= 99.5% (pinhole) / 99% (SPHERE) of pixels; after one black half-sweep >= 99.5% (pinhole) /
+      98.5% (SPHERE) of pixels hold the same plane, and the flips are near ties: their median cost gap
+      is below 1e-4.
+  T3  A full RunPatchMatch: >= 99% of finite depths within 1% of the exact mode's, ground-truth accuracy
+      within +-0.5 points.  Geom, planar-prior and hierarchy passes from one shared state: T3, T2's init
+      gates, and after one half-sweep >= 85% same plane (the hierarchy gate and the prior-restricted
+      acceptance multiply near ties; a flip there selects by restricted cost or pre-cost, so its cost gap
+      is not a tie measure and is not gated).
 """
 import numpy as np
 import pytest
@@ -38,18 +50,90 @@ def ctx():
     c.close()
 
 
-RIGS = {"pinhole": lambda: scene.pinhole_scene(320, 240, n_src=4, seed=5),
-        "sphere": lambda: scene.sphere_scene(640, 320, n_src=4, seed=3)}
-
-
-def run(ctx, mode, sc, p, seed, n_hs=-1, post=True):
+def run(ctx, mode, seed, n_hs=-1, post=True, setup=None):
     ctx.set_math(mode)
-    ctx.set_params(p)
-    ctx.upload_views(sc.images, sc.cameras)
+    setup(ctx)
     ctx.run_patchmatch(seed, n_half_sweeps=n_hs, do_post=post)
     pl, co = ctx.download()
     ctx.set_math("exact")
     return pl, co
+
+
+def plain_setup(sc, p):
+    def f(c):
+        c.set_params(p)
+        c.upload_views(sc.images, sc.cameras)
+    return f
+
+
+def near_surface_queries(sc, n, seed):
+    rng = np.random.default_rng(seed)
+    H, W = sc.images[0].shape
+    px, py = rng.integers(6, W - 6, n).astype(np.int32), rng.integers(6, H - 6, n).astype(np.int32)
+    planes = []
+    for k in range(n):
+        d = npr.pixel_to_dir(sc.cameras[0], int(px[k]), int(py[k]))
+        nrm = -d + rng.normal(0, 0.2, 3)
+        nrm /= np.linalg.norm(nrm)
+        depth = float(sc.gt_depth[py[k], px[k]]) * rng.uniform(0.98, 1.02)
+        planes.append([*nrm, -float(nrm @ (d * depth))])
+    return px, py, np.asarray(planes, np.float32)
+
+
+def check_t1(ctx, sc, p, n, seed, sphere):
+    V = len(sc.images) - 1
+    px, py, planes = near_surface_queries(sc, n, seed)
+    ctx.set_params(p)
+    ctx.upload_views(sc.images, sc.cameras)
+    ctx.set_math("fast")
+    f = ctx.debug_ncc(px, py, planes)
+    ctx.set_math("exact")
+    e = ctx.debug_ncc(px, py, planes)
+    ref = np.array([[npr.bilateral_ncc(sc.images, sc.cameras, p, v, int(px[k]), int(py[k]),
+                                       planes[k].astype(np.float64)) for v in range(1, V + 1)] for k in range(n)])
+    # (a) a cost of 2.0 is the reference's "no match" (centre outside, weight sum < 1e-6, variance
+    # < 1e-5) or a clamped NCC; its thresholds are discontinuities the binary32 noise can cross, so the
+    # fast mode may flip a query's class no more often than the exact mode's own class differs from
+    # float64's, and never by more than 1% of the queries
+    agree_fe = np.mean((f >= 2.0) == (e >= 2.0))
+    agree_ef = np.mean((e >= 2.0) == (ref >= 2.0))
+    assert agree_fe >= min(agree_ef, 0.999) - 0.002 and agree_fe >= 0.99, (agree_fe, agree_ef)
+    valid = (e < 2.0) & (f < 2.0) & (ref < 2.0)
+    assert valid.mean() > 0.3
+    df, de, dfe = np.abs(f - ref)[valid], np.abs(e - ref)[valid], np.abs(f - e)[valid]
+    if sphere:                                                                        # (b)
+        assert np.mean(dfe <= 1e-4) >= np.mean(de <= 1e-4) - 0.05, (np.mean(dfe <= 1e-4), np.mean(de <= 1e-4))
+    else:
+        assert np.mean(dfe <= 1e-4) >= 0.995, np.mean(dfe <= 1e-4)
+    fast_worse, exact_worse = np.mean(df > de + 1e-4), np.mean(de > df + 1e-4)        # (c)
+    assert fast_worse <= exact_worse + 0.03, (fast_worse, exact_worse)
+
+
+def check_t2(ctx, setup, seed, sphere, init=True, hs_min=None, gap_max=1e-4):
+    if init:
+        fp, fc = run(ctx, "fast", seed, 0, False, setup)
+        ep, ec = run(ctx, "exact", seed, 0, False, setup)
+        assert np.array_equal(fp.view(np.uint32), ep.view(np.uint32))                # RNG only
+        fin = np.isfinite(ec) & np.isfinite(fc)
+        assert np.mean(np.abs(fc - ec)[fin] <= 1e-3) >= (0.99 if sphere else 0.995)
+    fp, fc = run(ctx, "fast", seed, 1, False, setup)
+    ep, ec = run(ctx, "exact", seed, 1, False, setup)
+    same = np.all(np.abs(fp - ep) <= 1e-4 * np.maximum(1.0, np.abs(ep)), axis=-1)
+    floor = hs_min if hs_min is not None else (0.985 if sphere else 0.995)
+    assert same.mean() >= floor, same.mean()
+    fin = np.isfinite(fc) & np.isfinite(ec) & ~same
+    if gap_max is not None and fin.sum() > 20:
+        assert np.median(np.abs(fc - ec)[fin]) < gap_max, np.median(np.abs(fc - ec)[fin])
+
+
+def check_t3(ctx, setup, seed, gt):
+    fp, fc = run(ctx, "fast", seed, -1, True, setup)
+    ep, ec = run(ctx, "exact", seed, -1, True, setup)
+    fd, ed = fp[..., 3], ep[..., 3]
+    fin = np.isfinite(fd) & np.isfinite(ed) & (ed > 0)
+    assert np.mean(np.abs(fd - ed)[fin] <= 0.01 * ed[fin]) >= 0.99
+    acc_f, acc_e = scene.depth_accuracy(fd, gt), scene.depth_accuracy(ed, gt)
+    assert abs(acc_f - acc_e) <= 0.005, (acc_f, acc_e)
 
 
 def test_math_mode_switch(ctx):
@@ -61,74 +145,102 @@ def test_math_mode_switch(ctx):
         ctx._check(ctx.L.acmmp_set_math(ctx.h, 7), "set_math")
 
 
-@pytest.mark.parametrize("kind", ["pinhole", "sphere"])
-def test_t1_ncc_queries_within_float32_noise(ctx, kind):
-    sc = RIGS[kind]()
+# BASELINE.json configurations: the metric view, C2, C3 (at the 3200x1600 the
+# reference scheduler runs it at, k_eval_nb view-chunked), C5 with 20 sources, and V = 32 (the maximum).
+CONFIGS = {
+    "metric-sphere-2000x1500-v4": (lambda: scene.sphere_scene(2000, 1500, n_src=4, seed=1234, n_waves=24), 500, {}),
+    "c2-pinhole-1600x1200-v10": (lambda: scene.pinhole_scene(1600, 1200, n_src=10, seed=1234, n_waves=12), 300, {}),
+    "c3-sphere-3200x1600-v15": (lambda: scene.sphere_scene(3200, 1600, n_src=15, seed=1234, n_waves=12), 200,
+                                {"ACMMP_NB_VIEW_CHUNK": "8"}),
+    "c5-pinhole-1920x1080-v20": (lambda: scene.pinhole_scene(1920, 1080, n_src=20, seed=55, n_waves=12), 150, {}),
+    "pinhole-640x480-v32": (lambda: scene.pinhole_scene(640, 480, n_src=32, seed=32, n_waves=24), 100, {}),
+    "sphere-640x320-v32": (lambda: scene.sphere_scene(640, 320, n_src=32, seed=33, n_waves=24), 100, {}),
+}
+
+
+@pytest.fixture(scope="module", params=list(CONFIGS))
+def config(request):
+    make, nq, env = CONFIGS[request.param]
+    sc = make()
+    return request.param, sc, nq, env
+
+
+@pytest.mark.slow
+def test_fast_mode_tolerance_at_baseline_configs(ctx, config, monkeypatch):
+    name, sc, nq, env = config
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sphere = name.startswith(("metric", "c3", "sphere"))
     p = params_for(sc)
+    check_t1(ctx, sc, p, nq, seed=len(name), sphere=sphere)
+    setup = plain_setup(sc, p)
+    check_t2(ctx, setup, 81, sphere)
+    check_t3(ctx, setup, 82, sc.gt_depth)
+
+
+PASS_RIGS = {"pinhole": lambda: scene.pinhole_scene(800, 600, n_src=10, seed=61, n_waves=24),
+             "sphere": lambda: scene.sphere_scene(1000, 500, n_src=6, seed=62, n_waves=24)}
+
+
+@pytest.fixture(scope="module", params=list(PASS_RIGS))
+def pass_rig(request, ctx):
+    """A random first pass in the exact mode: the state the geom / planar / hierarchy passes start from."""
+    sc = PASS_RIGS[request.param]()
     H, W = sc.images[0].shape
-    rng = np.random.default_rng(1)
-    n = 250
-    px, py = rng.integers(6, W - 6, n).astype(np.int32), rng.integers(6, H - 6, n).astype(np.int32)
-    planes = []
-    for k in range(n):                         # planes near the ground-truth surface (well-matched costs)
-        d = npr.pixel_to_dir(sc.cameras[0], int(px[k]), int(py[k]))
-        nrm = -d + rng.normal(0, 0.2, 3)
-        nrm /= np.linalg.norm(nrm)
-        depth = float(sc.gt_depth[py[k], px[k]]) * rng.uniform(0.98, 1.02)
-        planes.append([*nrm, -float(nrm @ (d * depth))])
-    planes = np.asarray(planes, np.float32)
-    ctx.set_params(p)
-    ctx.upload_views(sc.images, sc.cameras)
-    ctx.set_math("fast")
-    fast = ctx.debug_ncc(px, py, planes)
+    V = len(sc.images) - 1
+    p0 = params_for(sc)
     ctx.set_math("exact")
-    exact = ctx.debug_ncc(px, py, planes)
-    ref = np.array([[npr.bilateral_ncc(sc.images, sc.cameras, p, v, int(px[k]), int(py[k]), planes[k].astype(np.float64))
-                     for v in range(1, 5)] for k in range(n)])
-    assert np.mean((fast >= 2.0) == (exact >= 2.0)) == 1.0
-    valid = (exact < 2.0) & (ref < 2.0)
-    assert valid.mean() > 0.5
-    ef, ee = np.abs(fast - ref)[valid], np.abs(exact - ref)[valid]
-    for q in (0.5, 0.99):
-        assert np.quantile(ef, q) <= np.quantile(ee, q) + 1e-4, (q, np.quantile(ef, q), np.quantile(ee, q))
-    d = np.abs(fast - exact)[valid]
-    if kind == "pinhole":
-        assert np.mean(d <= 1e-4) >= 0.995 and np.mean(d <= 1e-3) == 1.0
+    ctx.set_params(p0)
+    ctx.upload_views(sc.images, sc.cameras)
+    ctx.run_patchmatch(70)
+    first_p, first_c = ctx.download()
+    rng = np.random.default_rng(71)
+    depths = [first_p[..., 3]] + [(sc.gt_depth * rng.uniform(0.98, 1.02, (H, W))).astype(np.float32)
+                                  for _ in range(V)]
+    ctx.set_state(first_p, first_c)
+    ctx.set_planar_prior_from_maps(first_p[..., 3], first_c, float(p0["depth_min"]), float(p0["depth_max"]))
+    prior, masks = ctx.download_planar_prior()
+    return request.param, sc, first_p, first_c, depths, prior, masks
+
+
+@pytest.mark.parametrize("kind", ["geom", "planar", "hierarchy"])
+def test_fast_mode_tolerance_in_geom_planar_hierarchy_passes(ctx, pass_rig, kind):
+    model, sc, first_p, first_c, depths, prior, masks = pass_rig
+    H, W = sc.images[0].shape
+
+    if kind == "geom":
+        def setup(c):
+            c.set_params(params_for(sc, geom_consistency=1, max_iterations=2))
+            c.upload_views(sc.images, sc.cameras)
+            c.upload_depths(depths)
+            c.set_state(first_p, first_c)
+    elif kind == "planar":
+        def setup(c):
+            c.set_params(params_for(sc, planar_prior=1))
+            c.upload_views(sc.images, sc.cameras)
+            c.set_state(first_p, first_c)
+            c.set_planar_prior(prior, masks)
     else:
-        assert np.mean(d <= 1e-3) >= 0.99
+        h, w = H // 2, W // 2
+        coarse = np.zeros((h, w, 4), np.float32)
+        coarse[..., :3] = first_p[::2, ::2, :3][:h, :w]
+        coarse[..., 3] = first_c[::2, ::2][:h, :w]
+        cur = np.zeros((H, W, 4), np.float32)
+        cur[..., 3] = first_p[..., 3]
+        zc = np.zeros((H, W), np.float32)
 
-
-@pytest.mark.parametrize("kind", ["pinhole", "sphere"])
-def test_t2_same_winners(ctx, kind):
-    sc = RIGS[kind]()
-    p = params_for(sc)
-    fp, fc = run(ctx, "fast", sc, p, 5, n_hs=0, post=False)
-    ep, ec = run(ctx, "exact", sc, p, 5, n_hs=0, post=False)
-    assert np.array_equal(fp, ep)                                   # init planes: RNG only
-    fin = np.isfinite(ec)
-    assert np.mean(np.abs(fc - ec)[fin] <= 1e-3) >= 0.995
-    fp, fc = run(ctx, "fast", sc, p, 5, n_hs=1, post=False)
-    ep, ec = run(ctx, "exact", sc, p, 5, n_hs=1, post=False)
-    same = np.all(np.abs(fp - ep) <= 1e-4 * np.maximum(1.0, np.abs(ep)), axis=-1)
-    assert same.mean() >= 0.985, same.mean()
-
-
-@pytest.mark.parametrize("kind", ["pinhole", "sphere"])
-def test_t3_full_run_depths_and_accuracy(ctx, kind):
-    sc = RIGS[kind]()
-    p = params_for(sc)
-    fp, fc = run(ctx, "fast", sc, p, 9)
-    ep, ec = run(ctx, "exact", sc, p, 9)
-    fd, ed = fp[..., 3], ep[..., 3]
-    fin = np.isfinite(fd) & np.isfinite(ed) & (ed > 0)
-    assert np.mean(np.abs(fd - ed)[fin] <= 0.01 * ed[fin]) >= 0.99
-    acc_f, acc_e = scene.depth_accuracy(fd, sc.gt_depth), scene.depth_accuracy(ed, sc.gt_depth)
-    assert abs(acc_f - acc_e) <= 0.005, (acc_f, acc_e)
+        def setup(c):
+            c.set_params(params_for(sc, hierarchy=1, upsample=1, scaled_cols=w, scaled_rows=h))
+            c.upload_views(sc.images, sc.cameras)
+            c.set_state(cur, zc)
+            c.set_scaled_state(coarse)
+    check_t2(ctx, setup, 72, model == "sphere", init=True, hs_min=0.85, gap_max=None)
+    check_t3(ctx, setup, 73, sc.gt_depth)
 
 
 def test_fast_mode_is_deterministic(ctx):
-    sc = RIGS["sphere"]()
-    p = params_for(sc)
-    a = run(ctx, "fast", sc, p, 21)
-    b = run(ctx, "fast", sc, p, 21)
+    sc = scene.sphere_scene(640, 320, n_src=4, seed=3)
+    setup = plain_setup(sc, params_for(sc))
+    a = run(ctx, "fast", 21, setup=setup)
+    b = run(ctx, "fast", 21, setup=setup)
     assert np.array_equal(a[0], b[0], equal_nan=True) and np.array_equal(a[1], b[1], equal_nan=True)
