@@ -658,16 +658,6 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     }
     const int R = kp.R, inc = kp.inc;
     constexpr int G = PIPE ? VB : 1;
-    // PF (fast-mode SPHERE k_eval_nb chunks): the texels of sample s are consumed while sample s + 1's
-    // loads are in flight -- each wave keeps two samples' gathers outstanding, so the gather latency
-    // hides behind the next sample's projection instead of stalling the wave (same accumulation order)
-    constexpr bool PF = PIPE && FM && MODEL == kSphere && STAGED == 3;
-    Tap ptap[VB];
-    float pw = 0.f, pr = 0.f;
-    f32x2 pwwr = splat2(0.f);
-    bool pok[VB];
-#pragma unroll
-    for (int v = 0; v < VB; ++v) pok[v] = false;
     int s = 0, ii = 0;
     for (int i = -R; i <= R; i += inc, ++ii) {
         int jj = 0;                                      // s % nside without a division per sample
@@ -749,29 +739,12 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 if (FULL && MODEL == kSphere) __builtin_amdgcn_sched_barrier(0);
                 // G > 1: views are consumed in groups of G, a group's texels all in flight before the
                 // first is used (PIPE: the whole chunk; ~6 VGPRs per view in flight)
-                if (!PF && G > 1 && ((v + 1) % G == 0 || v == VB - 1)) {
+                if (G > 1 && ((v + 1) % G == 0 || v == VB - 1)) {
 #pragma unroll
                     for (int u = v - (v % G); u <= v; ++u)
                         if (has(u)) ACMMP_ACCUMULATE(u);
                 }
             }
-            if constexpr (PF) {
-                if (s > 0) {
-#pragma unroll
-                    for (int u = 0; u < VB; ++u)
-                        if (has(u)) ACMMP_ACCUMULATE_T(u, ptap[u], pw, pwwr, pr, pok[u]);
-                }
-#pragma unroll
-                for (int u = 0; u < VB; ++u) { ptap[u] = tap[u]; pok[u] = ok[u]; }
-                pw = w; pr = r; pwwr = wwr;
-            }
-        }
-    }
-    if constexpr (PF) {
-        if (s > 0) {
-#pragma unroll
-            for (int u = 0; u < VB; ++u)
-                if (has(u)) ACMMP_ACCUMULATE_T(u, ptap[u], pw, pwwr, pr, pok[u]);
         }
     }
 #undef ACMMP_ACCUMULATE
@@ -1473,12 +1446,12 @@ __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour
 // VGPRs spilled at the 64-VGPR budget; r02 A/B profiles/r02_split_nb_ab.txt: fast 388 -> 394, exact
 // 316.6 -> 320 Mpixel-iterations/s)
 template <int MODEL, int VB, int TEX, int FM>
-__global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? 5 : 8) : 1) void k_eval_nb(
+__global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? 7 : 8) : 1) void k_eval_nb(
     const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     // 8 lanes per pixel, one per neighbour direction (a pixel-major map -- a wave = 32 pixels x 2
-    // directions -- measured 3% slower, profiles/r03_ab1_packed_pixelmajor.txt)
+    // directions -- measured 3% slower, profiles/r03_eval_nb_ab.txt)
     const int lp = t / kNbLanes, h = t - lp * kNbLanes;
     const long long q = static_cast<long long>(blockIdx.x) * kNbPix + lp;
     int px = 0, py = 0;

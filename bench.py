@@ -84,12 +84,17 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true", help="skip the end-to-end ProcessProblem schedule timing")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_propagate.json"),
                     help="rocprofv3 PMC summary giving HBM bytes per propagation launch")
+    ap.add_argument("--timed-only", action="store_true",
+                    help="profiling: nothing runs on the GPU after the timed steps (no other math mode, latency, "
+                         "PCIe, variant, end-to-end or CPU legs), so a kernel trace's last launches are the timed ones")
     ap.add_argument("--allow-shared-gpus", action="store_true",
                     help="rehearsal only: let more ranks than GPUs share devices round-robin (never a scaling point)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch/rendezvous check: ranks join the gloo group, agree on the world and exit without "
                          "touching a GPU (the CPU test of `--gpus N`)")
     a = ap.parse_args()
+    if a.timed_only:
+        a.no_other_mode = a.no_cpu_baseline = a.no_variant = a.no_pipeline = True
     if a.gpus < 1:
         ap.error("--gpus must be >= 1")
     pipe = a.mode == "pipeline"        # BASELINE.json configs[3] shape vs the headline metric's
@@ -523,22 +528,24 @@ def main():
         ctx.set_math(args.math)
 
     planes, costs = ctx.download()
-    # per-map latency as the reference's RunPatchMatch ends (ACMMP.cu:1553-1554): run + D2H of planes
-    # and costs into caller-owned host buffers (inputs resident, as for `value`)
-    lat = []
-    for k in range(3):
+    d2h_ms = pcie_ms = None
+    if not args.timed_only:
+        # per-map latency as the reference's RunPatchMatch ends (ACMMP.cu:1553-1554): run + D2H of planes
+        # and costs into caller-owned host buffers (inputs resident, as for `value`)
+        lat = []
+        for k in range(3):
+            t1 = time.perf_counter()
+            ctx.run_patchmatch(args.seed + k)
+            ctx.download_into(planes, costs)
+            lat.append(time.perf_counter() - t1)
+        d2h_ms = float(np.median(lat)) * 1e3
+        # PCIe-inclusive rate (not `value`): host images in, RunPatchMatch, planes + costs back to the host --
+        # what a caller that hands over host buffers sees per depth map
         t1 = time.perf_counter()
-        ctx.run_patchmatch(args.seed + k)
-        ctx.download_into(planes, costs)
-        lat.append(time.perf_counter() - t1)
-    d2h_ms = float(np.median(lat)) * 1e3
-    # PCIe-inclusive rate (not `value`): host images in, RunPatchMatch, planes + costs back to the host --
-    # what a caller that hands over host buffers sees per depth map
-    t1 = time.perf_counter()
-    ctx.upload_views(sc.images, sc.cameras)
-    ctx.run_patchmatch(args.seed)
-    planes, costs = ctx.download()
-    pcie_ms = (time.perf_counter() - t1) * 1e3
+        ctx.upload_views(sc.images, sc.cameras)
+        ctx.run_patchmatch(args.seed)
+        planes, costs = ctx.download()
+        pcie_ms = (time.perf_counter() - t1) * 1e3
     nan_frac = float(np.isnan(costs).mean())
     acc = scene.depth_accuracy(planes[..., 3], sc.gt_depth)
 
@@ -599,11 +606,11 @@ def main():
     # the pipeline's one exchange step: after a pass every rank's depth map reaches every
     # other rank -- a grouped RCCL broadcast of each rank's map, HBM to HBM, outside the timed region
     exch = None
-    if world > 1 and ndev and world <= ndev and os.environ.get("ACMMP_BENCH_EXCHANGE", "1") != "0":
+    if world > 1 and ndev and world <= ndev and not args.timed_only and os.environ.get("ACMMP_BENCH_EXCHANGE", "1") != "0":
         exch = depth_exchange(args, ctx, rank, world, local_rank % ndev, dist, allmax)
     # the single-view latency mode: one view's rows split over the GPUs
     bsplit = None
-    if world > 1 and ndev and world <= ndev and os.environ.get("ACMMP_BENCH_BAND", "1") != "0":
+    if world > 1 and ndev and world <= ndev and not args.timed_only and os.environ.get("ACMMP_BENCH_BAND", "1") != "0":
         bsplit = band_split(args, rank, world, local_rank % ndev, dist, allmax)
 
     cpu = None
@@ -627,7 +634,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
-            "ms_per_depth_map": round(d2h_ms, 3),
+            "ms_per_depth_map": None if d2h_ms is None else round(d2h_ms, 3),
             "ms_per_depth_map_note": "one RunPatchMatch incl. the D2H of planes + costs (ACMMP.cu:1553-1554), "
                                      "inputs resident; ms_per_step is the same without the D2H",
             "higher_is_better": True,
@@ -644,9 +651,9 @@ def main():
             "stages_ms": {"init": round(stage[0] / args.steps, 3), "propagation": round(stage[1] / args.steps, 3),
                           "post": round(stage[2] / args.steps, 3)},
             "prop_only_mpix_per_s": round(P * args.iters * world / (stage[1] / args.steps * 1e-3) / 1e6, 3),
-            "pcie_inclusive": {"ms_per_depth_map": round(pcie_ms, 3),
-                               "mpix_iter_per_s": round(P * args.iters / (pcie_ms * 1e-3) / 1e6, 3),
-                               "note": "one rank: upload_views + run_patchmatch + download, host wall clock"},
+            "pcie_inclusive": None if pcie_ms is None else {
+                "ms_per_depth_map": round(pcie_ms, 3), "mpix_iter_per_s": round(P * args.iters / (pcie_ms * 1e-3) / 1e6, 3),
+                "note": "one rank: upload_views + run_patchmatch + download, host wall clock"},
             "quality": {"frac_within_1pct_gt": round(acc, 4), "nan_cost_frac": round(nan_frac, 4)},
             "roofline": roofline,
             "cpu_baseline": cpu,
