@@ -786,9 +786,10 @@ static unsigned long long colour_pixels(const acmmp_ctx* c, const KParams& kp, i
     return n;
 }
 
-// Split point of the refinement evaluation: about half the views, a multiple of the
-// 4-view NCC chunk above 4 views; 0 (no split) for one view, for colour grids too large for the
-// 32-bit queue entries, or with ACMMP_REF_SPLIT=0 in the environment (A/B switch).
+// Split point of the refinement evaluation: half the views up to 4 views, one 4-view NCC
+// chunk above (r03 sweep, profiles/r03_ref_split_sweep.txt / r03_ref_split_v20.txt: at V = 10, 15 and 20
+// S = 4 beats 6 / 8 / 12 by 1-4%); 0 (no split) for one view, for colour grids too large for the 32-bit
+// queue entries, or with ACMMP_REF_SPLIT=0 in the environment (A/B switch).
 // Read at every run (one getenv per RunPatchMatch), so tests can switch it within one process.
 static int ref_split_point(int V, size_t Pc) {
     const char* e_on = std::getenv("ACMMP_REF_SPLIT");
@@ -797,7 +798,7 @@ static int ref_split_point(int V, size_t Pc) {
     const int at = e_at ? std::atoi(e_at) : 0;
     if (!enabled || V < 2 || Pc >= (static_cast<size_t>(1) << 29)) return 0;
     if (at > 0) return at < V ? at : 0;
-    return V <= 4 ? V / 2 : 4 * std::max(1, (V / 2 + 2) / 4);
+    return V <= 4 ? V / 2 : 4;
 }
 
 static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
