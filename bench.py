@@ -228,6 +228,26 @@ def cpu_baseline(args, sc, params, gpu_rate_check=None):
     }
 
 
+def guarded(fn, seconds, *a):
+    """Run one of the multi-rank extras (first runs of the RCCL paths on a multi-GPU node) with a deadline:
+    its failure or hang must not cost the headline line.  Returns (result, abandoned); abandoned = a
+    worker thread may still be blocked in a collective, so the process must exit without tearing down."""
+    import threading
+    box = {}
+
+    def run():
+        try:
+            box["r"] = fn(*a)
+        except Exception as e:                               # noqa: BLE001 -- reported in the line
+            box["r"] = {"error": f"{type(e).__name__}: {e}"}
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    t.join(seconds)
+    if t.is_alive():
+        return {"error": f"no result within {seconds} s (abandoned)"}, True
+    return box["r"], False
+
+
 def depth_exchange(args, ctx, rank, world, device, dist, allmax, reps=5):
     """Every rank broadcasts its last depth map (W x H float32, acmmp_export_depth: HBM to HBM) to all
     ranks in one grouped RCCL call -- what pipeline.RcclExchange does between two passes.  The RCCL
@@ -605,13 +625,17 @@ def main():
 
     # the pipeline's one exchange step: after a pass every rank's depth map reaches every
     # other rank -- a grouped RCCL broadcast of each rank's map, HBM to HBM, outside the timed region
+    # (each under a deadline: a failed or hung first run of an RCCL path reports itself in the line)
     exch = None
+    abandoned = False
+    deadline = float(os.environ.get("ACMMP_BENCH_EXTRA_S", "180"))
     if world > 1 and ndev and world <= ndev and not args.timed_only and os.environ.get("ACMMP_BENCH_EXCHANGE", "1") != "0":
-        exch = depth_exchange(args, ctx, rank, world, local_rank % ndev, dist, allmax)
+        exch, abandoned = guarded(depth_exchange, deadline, args, ctx, rank, world, local_rank % ndev, dist, allmax)
     # the single-view latency mode: one view's rows split over the GPUs
     bsplit = None
-    if world > 1 and ndev and world <= ndev and not args.timed_only and os.environ.get("ACMMP_BENCH_BAND", "1") != "0":
-        bsplit = band_split(args, rank, world, local_rank % ndev, dist, allmax)
+    if (world > 1 and ndev and world <= ndev and not args.timed_only and not abandoned
+            and os.environ.get("ACMMP_BENCH_BAND", "1") != "0"):
+        bsplit, abandoned = guarded(band_split, deadline, args, rank, world, local_rank % ndev, dist, allmax)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -663,6 +687,12 @@ def main():
             "band_split": bsplit,
         }
         print(json.dumps(line), flush=True)
+    if abandoned:
+        # a worker thread is blocked inside a collective: leave without tearing down the process group or
+        # the context it uses (the headline line is out; every rank reaches this at the same deadline)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -60,3 +60,23 @@ def test_refuses_more_ranks_than_gpus():
 def test_launcher_world_mismatch_is_an_error():
     r = _bench("--gpus", "4", "--dry-run", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "launcher started 1" in r.stderr
+
+
+def test_multi_rank_extras_are_guarded():
+    """The first runs of the RCCL extras (depth_exchange, band_split) cannot cost the headline line: an
+    exception is reported in the line, and a hang is abandoned at the deadline."""
+    import importlib.util
+    import time
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+
+    def boom():
+        raise RuntimeError("rccl said no")
+    r, abandoned = bench.guarded(boom, 5)
+    assert not abandoned and "rccl said no" in r["error"]
+    r, abandoned = bench.guarded(lambda x: {"ok": x}, 5, 7)
+    assert r == {"ok": 7} and not abandoned
+    t0 = time.perf_counter()
+    r, abandoned = bench.guarded(time.sleep, 0.5, 30)
+    assert abandoned and "abandoned" in r["error"] and time.perf_counter() - t0 < 5
