@@ -14,7 +14,7 @@ for rep in 1 2; do
   for lib in $LIBS; do
     for m in fast exact; do
       ACMMP_LIB=$lib timeout -k 10 300 python bench.py $ARGS --math $m > $OUT/b.json 2> $OUT/b.err || { tail $OUT/b.err; exit 1; }
-      python -c "import json,os;d=json.load(open('$OUT/b.json'));print(os.path.basename('$lib'), '$m', d['value'], d['ms_per_step'], d['roofline']['half_sweep_kernels_ms'])" | tee -a $OUT/ab.txt
+      python -c "import json,os;d=json.load(open('$OUT/b.json'));print(os.path.basename('$lib'), '$m', d['value'], d['ms_per_step'], d['roofline']['half_sweep_kernels_ms'], d['stages_ms'])" | tee -a $OUT/ab.txt
     done
   done
 done
