@@ -98,6 +98,9 @@ struct acmmp_ctx {
     float4* d_prior = nullptr;
     uint32_t* d_mask = nullptr;
     size_t prior_cap = 0, mask_cap = 0;
+    // grow-only capacities of buffers refilled per call (a hipFree waits for the whole device, i.e. for
+    // every other context's kernels: reallocating per problem serialised the pipeline's contexts)
+    size_t dep_cap = 0, scaled_cap = 0, spatial_cap = 0;
     bool has_prior = false;           // set_planar_prior since the last upload_views
     char* d_pp = nullptr;             // planar-prior triangle tables (acmmp_set_planar_prior_from_maps)
     size_t pp_cap = 0;
@@ -648,14 +651,15 @@ static acmmp_status upload_depths(acmmp_ctx* c, int n, const float* const* depth
         off[i] = total;
         total += static_cast<size_t>(w[i]) * h[i];
     }
-    HIP_TRY(c, dalloc(c->d_dep, total));
+    HIP_TRY(c, dreserve(c->d_dep, c->dep_cap, total));
     for (int i = 0; i < c->N; ++i) {
-        HIP_TRY(c, hipMemcpy(c->d_dep + off[i], depths[i], sizeof(float) * w[i] * h[i], kind));
+        HIP_TRY(c, hipMemcpyAsync(c->d_dep + off[i], depths[i], sizeof(float) * w[i] * h[i], kind, c->stream));
         c->dcams[i].dep_off = static_cast<long long>(off[i]);
         c->dcams[i].dep_w = w[i];
         c->dcams[i].dep_h = h[i];
     }
-    HIP_TRY(c, hipMemcpy(c->d_cams, c->dcams.data(), sizeof(DevCam) * c->N, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpyAsync(c->d_cams, c->dcams.data(), sizeof(DevCam) * c->N, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));             // the sources may be reused once this returns
     c->has_depths = true;
     return ACMMP_OK;
 }
@@ -684,16 +688,19 @@ acmmp_status acmmp_set_state(acmmp_ctx* c, const float* planes, const float* cos
     if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
     HIP_TRY(c, hipSetDevice(c->device));
     const size_t P = P_of(c);
-    if (planes) HIP_TRY(c, hipMemcpy(c->d_planes_rm, planes, sizeof(float4) * P, hipMemcpyHostToDevice));
-    if (costs) HIP_TRY(c, hipMemcpy(c->d_costs_rm, costs, sizeof(float) * P, hipMemcpyHostToDevice));
+    if (planes)
+        HIP_TRY(c, hipMemcpyAsync(c->d_planes_rm, planes, sizeof(float4) * P, hipMemcpyHostToDevice, c->stream));
+    if (costs) HIP_TRY(c, hipMemcpyAsync(c->d_costs_rm, costs, sizeof(float) * P, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     return ACMMP_OK;
 }
 
 acmmp_status acmmp_set_scaled_state(acmmp_ctx* c, const float* planes, int sw, int sh) {
     if (!c || !planes || sw <= 0 || sh <= 0) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "bad scaled state");
     HIP_TRY(c, hipSetDevice(c->device));
-    HIP_TRY(c, dalloc(c->d_scaled, static_cast<size_t>(sw) * sh));
-    HIP_TRY(c, hipMemcpy(c->d_scaled, planes, sizeof(float4) * sw * sh, hipMemcpyHostToDevice));
+    HIP_TRY(c, dreserve(c->d_scaled, c->scaled_cap, static_cast<size_t>(sw) * sh));
+    HIP_TRY(c, hipMemcpyAsync(c->d_scaled, planes, sizeof(float4) * sw * sh, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     c->sw = sw;
     c->sh = sh;
     c->has_scaled = true;
@@ -707,8 +714,9 @@ acmmp_status acmmp_set_planar_prior(acmmp_ctx* c, const float* prior, const uint
     const size_t P = P_of(c);
     HIP_TRY(c, dreserve(c->d_prior, c->prior_cap, P));
     HIP_TRY(c, dreserve(c->d_mask, c->mask_cap, P));
-    HIP_TRY(c, hipMemcpy(c->d_prior, prior, sizeof(float4) * P, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(c->d_mask, masks, sizeof(uint32_t) * P, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpyAsync(c->d_prior, prior, sizeof(float4) * P, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_mask, masks, sizeof(uint32_t) * P, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     c->has_prior = true;
     return ACMMP_OK;
 }
@@ -854,7 +862,7 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
         c->dirs_R = R;
     }
     kp.color_den = 2.0f * p.sigma_color * p.sigma_color;
-    HIP_TRY(c, dalloc(c->d_spatial, static_cast<size_t>(c->model == kSphere ? c->H : 1) * kp.S));
+    HIP_TRY(c, dreserve(c->d_spatial, c->spatial_cap, static_cast<size_t>(c->model == kSphere ? c->H : 1) * kp.S));
     HIP_TRY(c, launch_spatial_table(kp, c->d_spatial, c->stream));
     // half-sweep scratch slab: carve the pieces of engine.h's KParams out of one allocation
     size_t off[13];
