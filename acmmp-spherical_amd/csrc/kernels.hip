@@ -581,6 +581,25 @@ __device__ __forceinline__ Patch make_patch(const KParams& kp, int px, int py) {
 // reference camera in registers across the loop (read per sample through the constant address space
 // instead: -3%, r01_v27).
 
+// The NCC of one view from its weighted sums (ACMMP.cu:500-516): sbw = sum w, srrr = (sum w r, sum w r r),
+// ssrs = (sum w s, sum w r s), sss = sum w s s
+__device__ __forceinline__ float ncc_cost(float sbw, f32x2 srrr, f32x2 ssrs, float sss) {
+    float out = 2.0f;
+    if (!(sbw < 1e-6f)) {
+        const float inv = 1.0f / sbw;
+        const float m_ref = srrr.x * inv, m_src = ssrs.x * inv;
+        const float e_rr = srrr.y * inv, e_ss = sss * inv, e_rs = ssrs.y * inv;
+        const float var_ref = fmaf(-m_ref, m_ref, e_rr);
+        const float var_src = fmaf(-m_src, m_src, e_ss);
+        if (!(var_ref < 1e-5f || var_src < 1e-5f)) {
+            const float covar = fmaf(-m_ref, m_src, e_rs);
+            const float ncc = 1.0f - covar / sqrtf(var_ref * var_src);
+            out = fmaxf(0.0f, fminf(2.0f, ncc));
+        }
+    }
+    return out;
+}
+
 template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM = 0, bool FULL = false>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv_rt, float (&cost)[VB]) {
@@ -646,7 +665,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     // fast-mode SPHERE k_eval_nb chunks hold each view's Ft in VGPRs across the loop (a VOP3 fma reads
     // one SGPR, so a translation in SGPRs costs a move per view-sample): k_eval_nb -1.3..-1.7%, metric +1%
     // (profiles/r02_ft_vgpr_ab.txt)
-    constexpr bool kFtV = FM && MODEL == kSphere && STAGED == 3;
+    constexpr bool kFtV = FM && MODEL == kSphere && STAGED == 3 && !(TEX == 1);
     float ftv[VB][3];
 #pragma unroll
     for (int v = 0; v < VB; ++v) {
@@ -658,91 +677,182 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     }
     const int R = kp.R, inc = kp.inc;
     constexpr int G = PIPE ? VB : 1;
-    int s = 0, ii = 0;
-    for (int i = -R; i <= R; i += inc, ++ii) {
-        int jj = 0;                                      // s % nside without a division per sample
-        const float2 cs = STAGED == 4 ? pt.col[ii] : make_float2(0.f, 0.f);
-        for (int j = -R; j <= R; j += inc, ++s, ++jj) {
-            float r;
-            float4 rw;
-            if (STAGED == 4) {                           // coop_patch_sep layout (SPHERE): ray_at's products
-                const float2 rs = pt.row[jj];
-                const float2 q = pt.wr[s];
-                rw = make_float4(rs.y * cs.x, -rs.x, rs.y * cs.y, q.x);
-                r = q.y;
-            } else if (STAGED == 3) {                    // coop_patch_nb layout
-                const float4 q = pt.rw[s * pt.stride];
-                if (MODEL == kSphere) {
-                    rw = make_float4(q.x, pt.rr[jj * pt.stride], q.y, q.z);
-                    r = q.w;
-                } else {
-                    rw = q;
-                    r = pt.rr[s * pt.stride];
-                }
-            } else {
-                rw = patch_sample<MODEL>(kp, px, py, s, i, j, pt.center, r);
-            }
-            const float w = rw.w;
-            // reference camera through the constant address space too: scalar loads per sample
-            // instead of 12 wave-uniform VGPRs held across the loop
-            float3 P;
-            const float dep = FM ? depth_from_plane_fast(ph, rw) : depth_from_plane(ph, rw);
-            if (FM)
-                P = cam_point_fast<MODEL>(ccams[0], px + i, py + j, dep, rw);
-            else if (!PIPE)
-                P = world_point_ray<MODEL>(ccams[0], px + i, py + j, dep, rw);
-            else
-                P = world_point_ray<MODEL>(rc, px + i, py + j, dep, rw);
-            const float wr = w * r;
-            const f32x2 wwr = (f32x2){w, wr};
-            Tap tap[VB];
-            bool ok[VB];
-            // accumulate view v's sample (ACMMP.cu:488-498): texel tap T of a sample with weight W_,
-            // (w, w r) = WWR_ and reference texel R_
+    // accumulate view v's sample (ACMMP.cu:488-498): texel tap T of a sample with weight W_,
+    // (w, w r) = WWR_ and reference texel R_
 #define ACMMP_ACCUMULATE_T(v, T, W_, WWR_, R_, OK_)                          \
-            do {                                                             \
-                const float sp = lerp_tap<TEX>(T);                           \
-                if (MODEL == kSphere ? has(v) : (OK_)) {                     \
-                    if (MODEL == kPinhole) {                                 \
-                        sbw[v] += (W_);                                      \
-                        srrr[v] = pk_fma(WWR_, splat2(R_), srrr[v]);         \
-                    }                                                        \
-                    ssrs[v] = pk_fma(WWR_, splat2(sp), ssrs[v]);             \
-                    const float ws = (W_) * sp;                              \
-                    sss[v] = fmaf(ws, sp, sss[v]);                           \
-                }                                                            \
-            } while (0)
+    do {                                                             \
+        const float sp = lerp_tap<TEX>(T);                           \
+        if (MODEL == kSphere ? has(v) : (OK_)) {                     \
+            if (MODEL == kPinhole) {                                 \
+                sbw[v] += (W_);                                      \
+                srrr[v] = pk_fma(WWR_, splat2(R_), srrr[v]);         \
+            }                                                        \
+            ssrs[v] = pk_fma(WWR_, splat2(sp), ssrs[v]);             \
+            const float ws = (W_) * sp;                              \
+            sss[v] = fmaf(ws, sp, sss[v]);                           \
+        }                                                            \
+    } while (0)
 #define ACMMP_ACCUMULATE(v) ACMMP_ACCUMULATE_T(v, tap[v], w, wwr, r, ok[v])
+    // Fast SPHERE k_eval_nb chunks with 6x6 samples: per view, the source coordinates come from 16 exact
+    // projections at the samples of patch columns / rows {0, 2, 3, 5} and, for the others, the 4-point
+    // Lagrange interpolation through them (columns 1 and 4 from the node columns, then rows 1 and 4 from
+    // the node rows): 16 projections instead of 36 per hypothesis and view.  x is interpolated as the
+    // offset from the first node (unwrapped across the seam; small numbers, little rounding) and wrapped
+    // per sample as usual.  In float64 the interpolated NCC is within 4.5e-5 of the projected one for
+    // every query tried at the metric (near-surface and random planes, profiles/r03_interp_feasibility.json),
+    // far inside the binary32 noise floor of DESIGN.md §2.4; the fast-mode gates of
+    // tests/test_gpu_fastmath.py hold unchanged (k_eval_nb 1.75 -> 1.51 ms, profiles/r03_interp_ab.txt).
+    // Views are the outer loop here, and a view's patch columns are taken 0, 2, 3, 5, 1, 4 (each node
+    // column as soon as its nodes are projected).
+    constexpr bool kInterp = FM && MODEL == kSphere && STAGED == 3 && TEX == 1;
+    bool interp_done = false;
+    if constexpr (kInterp) {
+        if (kp.nside == 6) {
+            interp_done = true;
+            // Lagrange weights of patch column / row 1 and 4 on the node columns / rows 0, 2, 3, 5
+            constexpr float kL1[4] = {0.26666667f, 1.3333334f, -0.6666667f, 0.06666667f};
+            constexpr float kL4[4] = {0.06666667f, -0.6666667f, 1.3333334f, 0.26666667f};
+            constexpr int kNode[4] = {0, 2, 3, 5};
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
-                ok[v] = false;
-                if (has(v)) {
-                    ConstCam& c = PCV(v);
-                    float sx, sy, sd;
-                    if (FM) project_fast<MODEL>(c, P, sx, sy, kFtV ? ftv[v] : nullptr);
-                    else project<MODEL>(c, P, sx, sy, sd);
-                    ok[v] = true;
-                    if (MODEL == kSphere) {
-                        sx = fmaf(-floorf(sx * c.invW), c.Wf, sx);
-                        sy = FM ? __builtin_amdgcn_fmed3f(sy, 0.0f, c.Hm1f) : clamp0(sy, c.Hm1f);
-                    } else {
-                        ok[v] = !(sx < 0.0f || sx >= c.Wf || sy < 0.0f || sy >= c.Hf);
-                    }
-                    const __amdgpu_buffer_rsrc_t rs = TEX == 1
-                        ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000)
-                        : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(c.img_base), 0, c.img_bytes, 0x00020000);
-                    tap[v] = fetch_tap<TEX, MODEL == kSphere>(rs, c, sx, sy);
-                    if (G == 1) ACMMP_ACCUMULATE(v);
-                }
-                // a full SPHERE chunk has no per-view branches; keep its views' code in view order
-                // (interleaved, their live ranges overlap and the 7-wave register budget spills)
-                if (FULL && MODEL == kSphere) __builtin_amdgcn_sched_barrier(0);
-                // G > 1: views are consumed in groups of G, a group's texels all in flight before the
-                // first is used (PIPE: the whole chunk; ~6 VGPRs per view in flight)
-                if (G > 1 && ((v + 1) % G == 0 || v == VB - 1)) {
+                if (!has(v)) continue;
+                ConstCam& c = PCV(v);
+                const __amdgpu_buffer_rsrc_t rs =
+                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000);
+                float x00 = 0.f, y00 = 0.f;                 // the first node's position (set below)
+                // one patch column's six samples from its four row nodes (x, y): the bilinear tap and the
+                // sums of ACMMP.cu:488-498
+                auto column = [&](int ci, const float (&nx)[4], const float (&ny)[4]) {
 #pragma unroll
-                    for (int u = v - (v % G); u <= v; ++u)
-                        if (has(u)) ACMMP_ACCUMULATE(u);
+                    for (int cj = 0; cj < 6; ++cj) {
+                        float x, y;
+                        if (cj == 0 || cj == 2 || cj == 3 || cj == 5) {
+                            const int b = cj == 0 ? 0 : (cj == 2 ? 1 : (cj == 3 ? 2 : 3));
+                            x = nx[b];
+                            y = ny[b];
+                        } else {
+                            const float* L = cj == 1 ? kL1 : kL4;
+                            x = fmaf(L[3], nx[3], fmaf(L[2], nx[2], fmaf(L[1], nx[1], L[0] * nx[0])));
+                            y = fmaf(L[3], ny[3], fmaf(L[2], ny[2], fmaf(L[1], ny[1], L[0] * ny[0])));
+                        }
+                        const float4 q = pt.rw[(ci * 6 + cj) * pt.stride];
+                        const float w = q.z, r = q.w;
+                        x += x00;
+                        x = fmaf(-floorf(x * c.invW), c.Wf, x);
+                        y = __builtin_amdgcn_fmed3f(y, 0.0f, c.Hm1f);
+                        const Tap t = fetch_tap<TEX, true>(rs, c, x, y);
+                        const f32x2 wwr = (f32x2){w, w * r};
+                        ACMMP_ACCUMULATE_T(v, t, w, wwr, r, true);
+                    }
+                };
+                // node columns in turn: project their four row nodes, take the column's samples, and add the
+                // column into the interpolated columns 1 and 4, which follow
+                float c1x[4] = {0.f, 0.f, 0.f, 0.f}, c1y[4] = {0.f, 0.f, 0.f, 0.f};
+                float c4x[4] = {0.f, 0.f, 0.f, 0.f}, c4y[4] = {0.f, 0.f, 0.f, 0.f};
+                // nodes as offsets from the first one (x unwrapped across the seam): small numbers, so the
+                // interpolation's rounding stays far below the positions' own
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    float nx[4], ny[4];
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const float4 q = pt.rw[(kNode[a] * 6 + kNode[b]) * pt.stride];
+                        const float4 rw = make_float4(q.x, pt.rr[kNode[b] * pt.stride], q.y, q.z);
+                        const float dep = depth_from_plane_fast(ph, rw);
+                        float x, y;
+                        project_fast<MODEL>(c, make_float3(rw.x * dep, rw.y * dep, rw.z * dep), x, y);
+                        if (a == 0 && b == 0) {
+                            x00 = x;
+                            nx[b] = 0.0f;
+                        } else {
+                            const float dx = x - x00;
+                            nx[b] = fmaf(-rintf(dx * c.invW), c.Wf, dx);
+                        }
+                        ny[b] = y;
+                        c1x[b] = fmaf(kL1[a], nx[b], c1x[b]);
+                        c1y[b] = fmaf(kL1[a], ny[b], c1y[b]);
+                        c4x[b] = fmaf(kL4[a], nx[b], c4x[b]);
+                        c4y[b] = fmaf(kL4[a], ny[b], c4y[b]);
+                    }
+                    column(kNode[a], nx, ny);
+                }
+                column(1, c1x, c1y);
+                column(4, c4x, c4y);
+                __builtin_amdgcn_sched_barrier(0);           // one view's nodes live at a time
+            }
+        }
+    }
+    if (!interp_done) {
+        int s = 0, ii = 0;
+        for (int i = -R; i <= R; i += inc, ++ii) {
+            int jj = 0;                                      // s % nside without a division per sample
+            const float2 cs = STAGED == 4 ? pt.col[ii] : make_float2(0.f, 0.f);
+            for (int j = -R; j <= R; j += inc, ++s, ++jj) {
+                float r;
+                float4 rw;
+                if (STAGED == 4) {                           // coop_patch_sep layout (SPHERE): ray_at's products
+                    const float2 rs = pt.row[jj];
+                    const float2 q = pt.wr[s];
+                    rw = make_float4(rs.y * cs.x, -rs.x, rs.y * cs.y, q.x);
+                    r = q.y;
+                } else if (STAGED == 3) {                    // coop_patch_nb layout
+                    const float4 q = pt.rw[s * pt.stride];
+                    if (MODEL == kSphere) {
+                        rw = make_float4(q.x, pt.rr[jj * pt.stride], q.y, q.z);
+                        r = q.w;
+                    } else {
+                        rw = q;
+                        r = pt.rr[s * pt.stride];
+                    }
+                } else {
+                    rw = patch_sample<MODEL>(kp, px, py, s, i, j, pt.center, r);
+                }
+                const float w = rw.w;
+                // reference camera through the constant address space too: scalar loads per sample
+                // instead of 12 wave-uniform VGPRs held across the loop
+                float3 P;
+                const float dep = FM ? depth_from_plane_fast(ph, rw) : depth_from_plane(ph, rw);
+                if (FM)
+                    P = cam_point_fast<MODEL>(ccams[0], px + i, py + j, dep, rw);
+                else if (!PIPE)
+                    P = world_point_ray<MODEL>(ccams[0], px + i, py + j, dep, rw);
+                else
+                    P = world_point_ray<MODEL>(rc, px + i, py + j, dep, rw);
+                const float wr = w * r;
+                const f32x2 wwr = (f32x2){w, wr};
+                Tap tap[VB];
+                bool ok[VB];
+#pragma unroll
+                for (int v = 0; v < VB; ++v) {
+                    ok[v] = false;
+                    if (has(v)) {
+                        ConstCam& c = PCV(v);
+                        float sx, sy, sd;
+                        if (FM) project_fast<MODEL>(c, P, sx, sy, kFtV ? ftv[v] : nullptr);
+                        else project<MODEL>(c, P, sx, sy, sd);
+                        ok[v] = true;
+                        if (MODEL == kSphere) {
+                            sx = fmaf(-floorf(sx * c.invW), c.Wf, sx);
+                            sy = FM ? __builtin_amdgcn_fmed3f(sy, 0.0f, c.Hm1f) : clamp0(sy, c.Hm1f);
+                        } else {
+                            ok[v] = !(sx < 0.0f || sx >= c.Wf || sy < 0.0f || sy >= c.Hf);
+                        }
+                        const __amdgpu_buffer_rsrc_t rs = TEX == 1
+                            ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000)
+                            : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(c.img_base), 0, c.img_bytes, 0x00020000);
+                        tap[v] = fetch_tap<TEX, MODEL == kSphere>(rs, c, sx, sy);
+                        if (G == 1) ACMMP_ACCUMULATE(v);
+                    }
+                    // a full SPHERE chunk has no per-view branches; keep its views' code in view order
+                    // (interleaved, their live ranges overlap and the 7-wave register budget spills)
+                    if (FULL && MODEL == kSphere) __builtin_amdgcn_sched_barrier(0);
+                    // G > 1: views are consumed in groups of G, a group's texels all in flight before the
+                    // first is used (PIPE: the whole chunk; ~6 VGPRs per view in flight)
+                    if (G > 1 && ((v + 1) % G == 0 || v == VB - 1)) {
+#pragma unroll
+                        for (int u = v - (v % G); u <= v; ++u)
+                            if (has(u)) ACMMP_ACCUMULATE(u);
+                    }
                 }
             }
         }
@@ -750,22 +860,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
 #undef ACMMP_ACCUMULATE
 #undef ACMMP_ACCUMULATE_T
 #pragma unroll
-    for (int v = 0; v < VB; ++v) {
-        float out = 2.0f;
-        if (cval[v] && !(sbw[v] < 1e-6f)) {
-            const float inv = 1.0f / sbw[v];
-            const float m_ref = srrr[v].x * inv, m_src = ssrs[v].x * inv;
-            const float e_rr = srrr[v].y * inv, e_ss = sss[v] * inv, e_rs = ssrs[v].y * inv;
-            const float var_ref = fmaf(-m_ref, m_ref, e_rr);
-            const float var_src = fmaf(-m_src, m_src, e_ss);
-            if (!(var_ref < 1e-5f || var_src < 1e-5f)) {
-                const float covar = fmaf(-m_ref, m_src, e_rs);
-                const float ncc = 1.0f - covar / sqrtf(var_ref * var_src);
-                out = fmaxf(0.0f, fminf(2.0f, ncc));
-            }
-        }
-        cost[v] = out;
-    }
+    for (int v = 0; v < VB; ++v) cost[v] = cval[v] ? ncc_cost(sbw[v], srrr[v], ssrs[v], sss[v]) : 2.0f;
 #undef PCV
 }
 
