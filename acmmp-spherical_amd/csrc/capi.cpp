@@ -831,6 +831,11 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.model = c->model;
     kp.W = c->W; kp.H = c->H; kp.Wh = Wh_of(c); kp.N = c->N; kp.V = c->N - 1;
     kp.R = R; kp.inc = p.radius_increment; kp.nside = nside; kp.S = nside * nside;
+    // interpolated SPHERE sample coordinates in the fast k_eval_nb: 6x6 patches, and
+    // reference pixels of at most 2 pi / 1600 rad -- below that the patch's angular span makes the
+    // interpolation's float64 NCC error exceed 1e-4 in the tail (scripts/interp_feasibility.py; at
+    // 1600x800 the largest error is 6.7e-5, at 1280x640 8.5e-3)
+    kp.interp = c->model == kSphere && nside == 6 && c->W >= 1600 && c->H >= 800;
     kp.rows = std::min(c->H, 32 * (((c->H / 2) + 15) / 16));
     kp.row_lo = 0; kp.row_hi = kp.rows;
     kp.init_lo = 0; kp.init_hi = c->H;

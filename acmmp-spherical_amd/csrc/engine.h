@@ -82,6 +82,7 @@ struct KParams {
     int fast;                       // 1: fast-math NCC sample projection (acmmp_set_math)
     int W, H, Wh, N, V;             // ref size, colour row width ceil(W/2), images, source views
     int R, inc, nside, S;           // patch radius, radius_increment, offsets per axis, samples
+    int interp;                     // fast SPHERE k_eval_nb interpolates sample coordinates
     int rows;                       // rows the reference's checkerboard grid covers
     // row ranges (full image by default; a row band in the split latency mode, acmmp_band_*):
     int row_lo, row_hi;             // colour-grid rows the half-sweep kernels update, within [0, rows)

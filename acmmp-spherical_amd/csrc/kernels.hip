@@ -707,7 +707,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     constexpr bool kInterp = FM && MODEL == kSphere && STAGED == 3 && TEX == 1;
     bool interp_done = false;
     if constexpr (kInterp) {
-        if (kp.nside == 6) {
+        if (kp.interp) {
             interp_done = true;
             // Lagrange weights of patch column / row 1 and 4 on the node columns / rows 0, 2, 3, 5
             constexpr float kL1[4] = {0.26666667f, 1.3333334f, -0.6666667f, 0.06666667f};
