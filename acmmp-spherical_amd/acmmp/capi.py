@@ -30,7 +30,7 @@ EXPORTS = [
     "acmmp_debug_ncc", "acmmp_debug_geom",
     "acmmp_support_points", "acmmp_delaunay", "acmmp_prior_plane_params", "acmmp_depth_from_plane_param",
     "acmmp_planar_prior_host", "acmmp_set_planar_prior_from_maps", "acmmp_download_planar_prior",
-    "acmmp_upload_depths_device", "acmmp_upload_views_device", "acmmp_export_depth", "acmmp_device_alloc", "acmmp_device_free", "acmmp_memcpy",
+    "acmmp_upload_depths_device", "acmmp_upload_views_device", "acmmp_export_depth", "acmmp_export_state", "acmmp_set_state_device", "acmmp_device_alloc", "acmmp_device_free", "acmmp_memcpy",
     "acmmp_comm_unique_id", "acmmp_comm_create", "acmmp_comm_destroy", "acmmp_comm_broadcast",
     "acmmp_comm_allreduce_max", "acmmp_comm_band_exchange", "acmmp_run_patchmatch_band",
     "acmmp_band_begin", "acmmp_band_sweep", "acmmp_band_sweeps_left", "acmmp_band_halo_ranges",
@@ -95,6 +95,8 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_upload_depths_device.argtypes = [vp, i32, vp, vp, vp]
     L.acmmp_upload_views_device.argtypes = [vp, i32, vp, vp, vp]
     L.acmmp_export_depth.argtypes = [vp, vp]
+    L.acmmp_export_state.argtypes = [vp, vp, vp]
+    L.acmmp_set_state_device.argtypes = [vp, vp, vp]
     L.acmmp_device_alloc.argtypes = [i32, C.c_size_t, C.POINTER(vp)]
     L.acmmp_device_free.argtypes = [i32, vp]
     L.acmmp_memcpy.argtypes = [i32, vp, vp, C.c_size_t, i32]
@@ -298,6 +300,23 @@ class Context:
         if co is not None:
             self._check_hw(co, (), "set_state costs")
         self._check(self.L.acmmp_set_state(self.h, _p(pl), _p(co)), "set_state")
+
+    def export_state(self, planes_buf=None, costs_buf=None):
+        """Copy the last run's planes into DeviceBuffer `planes_buf` (H x W x 4) and its costs into
+        `costs_buf` (H x W), HBM to HBM."""
+        for b, tail, what in ((planes_buf, (4,), "planes"), (costs_buf, (), "costs")):
+            if b is not None and b.shape != (self.H, self.W) + tail:
+                raise ValueError(f"export_state {what}: buffer shape {b.shape}, expected {(self.H, self.W) + tail}")
+        self._check(self.L.acmmp_export_state(self.h, C.c_void_p(planes_buf.ptr if planes_buf else None),
+                                              C.c_void_p(costs_buf.ptr if costs_buf else None)), "export_state")
+
+    def set_state_device(self, planes_buf=None, costs_buf=None):
+        """set_state from DeviceBuffers of this context's GPU (shapes as export_state)."""
+        for b, tail, what in ((planes_buf, (4,), "planes"), (costs_buf, (), "costs")):
+            if b is not None and b.shape != (self.H, self.W) + tail:
+                raise ValueError(f"set_state_device {what}: buffer shape {b.shape}, expected {(self.H, self.W) + tail}")
+        self._check(self.L.acmmp_set_state_device(self.h, C.c_void_p(planes_buf.ptr if planes_buf else None),
+                                                  C.c_void_p(costs_buf.ptr if costs_buf else None)), "set_state_device")
 
     def set_scaled_state(self, planes):
         pl = np.ascontiguousarray(planes, np.float32)

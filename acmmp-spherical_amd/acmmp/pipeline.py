@@ -329,6 +329,7 @@ class Pipeline:
         # pass's downloaded plane array: keep it instead of re-joining the two stored maps
         self.reuse_planes = reuse_planes
         self._last_planes = {}                              # view -> (H, W, 4) planes of its last pass
+        self._dev_state = {}                                # view -> (planes, costs) DeviceBuffers of its last pass
         self.exchange = exchange or LocalExchange()
         self.world, self.rank = self.exchange.world, self.exchange.rank
         if self.world > 1 and order == "reference":
@@ -391,6 +392,10 @@ class Pipeline:
         if self.image_cache is not None:
             self.image_cache.close()
             self.image_cache = None
+        for dev in self._dev_state.values():
+            for b in dev:
+                b.free()
+        self._dev_state = {}
 
     # -- sharding
     def owner(self, i: int) -> int:
@@ -594,6 +599,10 @@ class Pipeline:
             self.store.put("normals", ref, planes[..., :3])
             self.store.put("costs", ref, costs)
             self._last_planes[ref] = planes
+            if self.reuse_planes and self.store.device is not None and isinstance(e, capi.Context):
+                # the same planes and costs kept in HBM too: the next geom pass restarts from them device
+                # to device (set_state_device) instead of uploading them from the host again
+                e.export_state(*self._state_buffers(ref, costs.shape))
             if self.out_folder:
                 d = os.path.join(self.out_folder, "ACMMP", f"2333_{ref:08d}")
                 os.makedirs(d, exist_ok=True)
@@ -601,6 +610,17 @@ class Pipeline:
                 io.write_dmb(os.path.join(d, "normals.dmb"), planes[..., :3])
                 io.write_dmb(os.path.join(d, "costs.dmb"), costs)
         return planes, costs
+
+    def _state_buffers(self, ref, shape):
+        """The HBM copy of view `ref`'s last planes and costs (allocated once per view and size)."""
+        dev = self._dev_state.get(ref)
+        if dev is None or dev[1].shape != tuple(shape):
+            if dev is not None:
+                for b in dev:
+                    b.free()
+            dev = (capi.DeviceBuffer(self.store.device, (*shape, 4)), capi.DeviceBuffer(self.store.device, shape))
+            self._dev_state[ref] = dev
+        return dev
 
     def _upload(self, e, p, images, cams, ids, ref, geom, hier, H, W):
         """InuputInitialization + the state reloads of ProcessProblem (ACMMP.cpp:567-679, 772-843)."""
@@ -613,8 +633,13 @@ class Pipeline:
                 e.upload_depths_device([self.store.device_map(key, v) for v in ids])
             else:
                 e.upload_depths([self.store.get(key, v) for v in ids])
-            costs = self.store.get("costs", ref)
             planes = self._last_planes.get(ref) if self.reuse_planes else None
+            dev = self._dev_state.get(ref)
+            if (planes is not None and planes.shape[:2] == (H, W) and dev is not None and dev[1].shape == (H, W)
+                    and hasattr(e, "set_state_device")):
+                e.set_state_device(*dev)
+                return
+            costs = self.store.get("costs", ref)
             if planes is None or planes.shape[:2] != (H, W):
                 depth = self.store.get(key, ref)
                 normals = self.store.get("normals", ref)

@@ -695,6 +695,32 @@ acmmp_status acmmp_set_state(acmmp_ctx* c, const float* planes, const float* cos
     return ACMMP_OK;
 }
 
+acmmp_status acmmp_export_state(acmmp_ctx* c, float* dev_planes, float* dev_costs) {
+    if (!c || (!dev_planes && !dev_costs)) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
+    if (!c->d_planes_rm) return fail(c, ACMMP_ERR_STATE, "no result yet");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t P = P_of(c);
+    if (dev_planes)
+        HIP_TRY(c, hipMemcpyAsync(dev_planes, c->d_planes_rm, sizeof(float4) * P, hipMemcpyDeviceToDevice, c->stream));
+    if (dev_costs)
+        HIP_TRY(c, hipMemcpyAsync(dev_costs, c->d_costs_rm, sizeof(float) * P, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));           // another context may read the buffers next
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_set_state_device(acmmp_ctx* c, const float* dev_planes, const float* dev_costs) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t P = P_of(c);
+    if (dev_planes)
+        HIP_TRY(c, hipMemcpyAsync(c->d_planes_rm, dev_planes, sizeof(float4) * P, hipMemcpyDeviceToDevice, c->stream));
+    if (dev_costs)
+        HIP_TRY(c, hipMemcpyAsync(c->d_costs_rm, dev_costs, sizeof(float) * P, hipMemcpyDeviceToDevice, c->stream));
+    // stream-ordered before this context's next kernels; the caller keeps the buffers until its run
+    return ACMMP_OK;
+}
+
 acmmp_status acmmp_set_scaled_state(acmmp_ctx* c, const float* planes, int sw, int sh) {
     if (!c || !planes || sw <= 0 || sh <= 0) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "bad scaled state");
     HIP_TRY(c, hipSetDevice(c->device));

@@ -30,6 +30,9 @@
 #define ACMMP_TU -1
 #endif
 #define ACMMP_IN_TU(n) (ACMMP_TU < 0 || ACMMP_TU == (n))
+#ifndef ACMMP_REF_INTERP
+#define ACMMP_REF_INTERP 0
+#endif
 
 namespace acmmp {
 
@@ -702,8 +705,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     // every query tried at the metric (near-surface and random planes, profiles/r03_interp_feasibility.json),
     // far inside the binary32 noise floor of DESIGN.md §2.4; the fast-mode gates of
     // tests/test_gpu_fastmath.py hold unchanged (k_eval_nb 1.75 -> 1.51 ms, profiles/r03_interp_ab.txt).
-    // Views are the outer loop here, and a view's patch columns are taken 0, 2, 3, 5, 1, 4 (each node
-    // column as soon as its nodes are projected).
+    // Views are the outer loop here, and a view's patch columns are taken 0, 2, 3, 5, 1, 4.
     constexpr bool kInterp = FM && MODEL == kSphere && STAGED == 3 && TEX == 1;
     bool interp_done = false;
     if constexpr (kInterp) {
@@ -719,7 +721,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 ConstCam& c = PCV(v);
                 const __amdgpu_buffer_rsrc_t rs =
                     __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000);
-                float x00 = 0.f, y00 = 0.f;                 // the first node's position (set below)
+                float x00 = 0.f;                            // the first node's x (set below)
                 // one patch column's six samples from its four row nodes (x, y): the bilinear tap and the
                 // sums of ACMMP.cu:488-498
                 auto column = [&](int ci, const float (&nx)[4], const float (&ny)[4]) {
@@ -745,15 +747,14 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         ACMMP_ACCUMULATE_T(v, t, w, wwr, r, true);
                     }
                 };
-                // node columns in turn: project their four row nodes, take the column's samples, and add the
-                // column into the interpolated columns 1 and 4, which follow
-                float c1x[4] = {0.f, 0.f, 0.f, 0.f}, c1y[4] = {0.f, 0.f, 0.f, 0.f};
-                float c4x[4] = {0.f, 0.f, 0.f, 0.f}, c4y[4] = {0.f, 0.f, 0.f, 0.f};
-                // nodes as offsets from the first one (x unwrapped across the seam): small numbers, so the
-                // interpolation's rounding stays far below the positions' own
+                // the view's 16 nodes first -- independent projections the scheduler interleaves (r03 A/B
+                // against projecting each node column just before its samples: k_eval_nb -1%, 2 VGPRs spilled
+                // instead of 4, profiles/r03_interp_form_ab.txt) -- with x as offsets from the first node,
+                // unwrapped across the seam: small numbers, so the interpolation's rounding stays far below
+                // the positions' own
+                float nx[4][4], ny[4][4];
 #pragma unroll
                 for (int a = 0; a < 4; ++a) {
-                    float nx[4], ny[4];
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
                         const float4 q = pt.rw[(kNode[a] * 6 + kNode[b]) * pt.stride];
@@ -763,18 +764,29 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         project_fast<MODEL>(c, make_float3(rw.x * dep, rw.y * dep, rw.z * dep), x, y);
                         if (a == 0 && b == 0) {
                             x00 = x;
-                            nx[b] = 0.0f;
+                            nx[a][b] = 0.0f;
                         } else {
                             const float dx = x - x00;
-                            nx[b] = fmaf(-rintf(dx * c.invW), c.Wf, dx);
+                            nx[a][b] = fmaf(-rintf(dx * c.invW), c.Wf, dx);
                         }
-                        ny[b] = y;
-                        c1x[b] = fmaf(kL1[a], nx[b], c1x[b]);
-                        c1y[b] = fmaf(kL1[a], ny[b], c1y[b]);
-                        c4x[b] = fmaf(kL4[a], nx[b], c4x[b]);
-                        c4y[b] = fmaf(kL4[a], ny[b], c4y[b]);
+                        ny[a][b] = y;
                     }
-                    column(kNode[a], nx, ny);
+                }
+#pragma unroll
+                for (int a = 0; a < 4; ++a) column(kNode[a], nx[a], ny[a]);
+                // the interpolated columns 1 and 4 at the node rows, formed after the node columns (fewer
+                // values live across them)
+                float c1x[4], c1y[4], c4x[4], c4y[4];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    c1x[b] = c1y[b] = c4x[b] = c4y[b] = 0.f;
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) {
+                        c1x[b] = fmaf(kL1[a], nx[a][b], c1x[b]);
+                        c1y[b] = fmaf(kL1[a], ny[a][b], c1y[b]);
+                        c4x[b] = fmaf(kL4[a], nx[a][b], c4x[b]);
+                        c4y[b] = fmaf(kL4[a], ny[a][b], c4y[b]);
+                    }
                 }
                 column(1, c1x, c1y);
                 column(4, c4x, c4y);
@@ -1903,7 +1915,7 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
 
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
 template <int MODEL, int VB, bool GEOM, int TF>
-__global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int colour) {
+__global__ __launch_bounds__(256, (ACMMP_REF_INTERP && MODEL == kSphere && TF == 2) ? 5 : 1) void k_eval_ref(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
@@ -1920,7 +1932,7 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
         vw = st.vw;
         weight_norm = st.weight_norm;
     }
-    constexpr int kStaged = (MODEL == kSphere && VB <= 4) ? 4 : 3;
+    constexpr int kStaged = (MODEL == kSphere && VB <= 4) ? ((ACMMP_REF_INTERP && TF == 2) ? 3 : 4) : 3;
     Patch pt;
     if constexpr (kStaged == 4) pt = coop_patch_sep<kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
     else pt = coop_patch_nb<MODEL, kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
@@ -2396,8 +2408,8 @@ hipError_t launch_select(const KParams& kp, int colour, int iter, hipStream_t s)
 #if ACMMP_IN_TU(4)
 hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s) {
     const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
-    const size_t lds_ref = (kp.model == kSphere && pick_vb(kp.V) <= 4) ? sep_lds_bytes(kp.S, kp.nside, kRefPix)
-                                                                       : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
+    const bool sep = kp.model == kSphere && pick_vb(kp.V) <= 4 && !(ACMMP_REF_INTERP && tf_of(kp) == 2);
+    const size_t lds_ref = sep ? sep_lds_bytes(kp.S, kp.nside, kRefPix) : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
     hipError_t e = hipSuccess;
     if (kp.ref_split > 0 && (e = hipMemsetAsync(kp.surv_count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
     const dim3 grd_ref = static_cast<unsigned>(cdiv(npix, kRefPix));

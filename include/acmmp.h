@@ -159,6 +159,12 @@ acmmp_status acmmp_export_depth(acmmp_ctx *ctx, float *dev_dst);
  * costs = P floats (may be NULL -> unchanged).  P = cams[0].width*height. */
 acmmp_status acmmp_set_state(acmmp_ctx *ctx, const float *planes, const float *costs);
 
+/* The last run's planes (P float4) and costs (P floats) copied into device buffers of this context's GPU
+ * (either may be NULL), and acmmp_set_state from such buffers: a geom pass restarts from the previous
+ * pass's state without the host round trip of ProcessProblem's .dmb reload (ACMMP.cpp:772-785). */
+acmmp_status acmmp_export_state(acmmp_ctx *ctx, float *dev_planes, float *dev_costs);
+acmmp_status acmmp_set_state_device(acmmp_ctx *ctx, const float *dev_planes, const float *dev_costs);
+
 /* Hierarchy coarse state scaled_plane_hypotheses (ACMMP.cpp:804-842):
  * sw*sh float4 row-major. */
 acmmp_status acmmp_set_scaled_state(acmmp_ctx *ctx, const float *planes, int sw, int sh);

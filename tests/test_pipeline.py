@@ -9,7 +9,7 @@ import socket
 import numpy as np
 import pytest
 
-from acmmp import io, pipeline
+from acmmp import io, pipeline, types
 from conftest import assert_bitwise_equal
 from pipeline_support import GlooExchange, OracleEngine, final_maps, small_dataset
 
@@ -185,6 +185,48 @@ def test_gpu_export_and_device_depth_upload_roundtrip():
         dev = pipe.store.dev[("depths_geom", v)].download()
         assert_bitwise_equal(dev, host, f"view {v}")
     assert isinstance(pipe.engine, capi.Context)
+
+
+@pytest.mark.gpu
+def test_gpu_device_state_restart_equals_host_upload():
+    """A geom pass restarted from the state kept in HBM (export_state -> set_state_device) equals the same
+    pass restarted from host planes / costs (set_state), bit for bit, in both math modes."""
+    from acmmp import capi
+    ds = small_dataset(64, 32, 3)
+    for math in ("exact", "fast"):
+        with capi.Context(0) as e:
+            e.set_math(math)
+            ids = [0, 1, 2]
+            p = types.default_params(num_images=3, depth_min=float(ds.cameras[0]["depth_min"]) * 0.6,
+                                     depth_max=float(ds.cameras[0]["depth_max"]) * 1.2)
+            e.set_params(p)
+            e.upload_views([ds.images[i] for i in ids], np.array([ds.cameras[i] for i in ids]))
+            e.run_patchmatch(5)
+            planes, costs = e.download()
+            bp, bc = capi.DeviceBuffer(0, (32, 64, 4)), capi.DeviceBuffer(0, (32, 64))
+            e.export_state(bp, bc)
+            assert_bitwise_equal(bp.download(), planes, "exported planes")
+            assert_bitwise_equal(bc.download(), costs, "exported costs")
+            dep = capi.DeviceBuffer(0, (32, 64))
+            e.export_depth(dep)
+            g = p.copy()
+            g["geom_consistency"] = 1
+            g["max_iterations"] = 2
+            outs = []
+            for via_device in (False, True):
+                e.set_params(g)
+                e.upload_views([ds.images[i] for i in ids], np.array([ds.cameras[i] for i in ids]))
+                e.upload_depths_device([dep, dep, dep])
+                if via_device:
+                    e.set_state_device(bp, bc)
+                else:
+                    e.set_state(planes, costs)
+                e.run_patchmatch(6)
+                outs.append(e.download())
+            assert_bitwise_equal(outs[1][0], outs[0][0], f"{math} planes")
+            assert_bitwise_equal(outs[1][1], outs[0][1], f"{math} costs")
+            for b in (bp, bc, dep):
+                b.free()
 
 
 def test_dense_folder_roundtrip(tmp_path):
