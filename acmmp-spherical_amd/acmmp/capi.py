@@ -301,20 +301,26 @@ class Context:
             self._check_hw(co, (), "set_state costs")
         self._check(self.L.acmmp_set_state(self.h, _p(pl), _p(co)), "set_state")
 
+    def _check_state_bufs(self, planes_buf, costs_buf, what):
+        # (H, W, 4) / (H, W) buffers, or larger flat ones (a view's buffers sized for its finest scale)
+        for b, k, name in ((planes_buf, 4, "planes"), (costs_buf, 1, "costs")):
+            if b is None:
+                continue
+            need = 4 * k * self.H * self.W
+            if b.shape != ((self.H, self.W, 4) if k == 4 else (self.H, self.W)) and (len(b.shape) != 1 or b.nbytes < need):
+                raise ValueError(f"{what} {name}: buffer shape {b.shape}, expected {(self.H, self.W)}"
+                                 f"{' + (4,)' if k == 4 else ''} or a flat buffer of at least {need} bytes")
+
     def export_state(self, planes_buf=None, costs_buf=None):
         """Copy the last run's planes into DeviceBuffer `planes_buf` (H x W x 4) and its costs into
         `costs_buf` (H x W), HBM to HBM."""
-        for b, tail, what in ((planes_buf, (4,), "planes"), (costs_buf, (), "costs")):
-            if b is not None and b.shape != (self.H, self.W) + tail:
-                raise ValueError(f"export_state {what}: buffer shape {b.shape}, expected {(self.H, self.W) + tail}")
+        self._check_state_bufs(planes_buf, costs_buf, "export_state")
         self._check(self.L.acmmp_export_state(self.h, C.c_void_p(planes_buf.ptr if planes_buf else None),
                                               C.c_void_p(costs_buf.ptr if costs_buf else None)), "export_state")
 
     def set_state_device(self, planes_buf=None, costs_buf=None):
         """set_state from DeviceBuffers of this context's GPU (shapes as export_state)."""
-        for b, tail, what in ((planes_buf, (4,), "planes"), (costs_buf, (), "costs")):
-            if b is not None and b.shape != (self.H, self.W) + tail:
-                raise ValueError(f"set_state_device {what}: buffer shape {b.shape}, expected {(self.H, self.W) + tail}")
+        self._check_state_bufs(planes_buf, costs_buf, "set_state_device")
         self._check(self.L.acmmp_set_state_device(self.h, C.c_void_p(planes_buf.ptr if planes_buf else None),
                                                   C.c_void_p(costs_buf.ptr if costs_buf else None)), "set_state_device")
 

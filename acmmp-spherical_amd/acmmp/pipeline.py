@@ -329,7 +329,7 @@ class Pipeline:
         # pass's downloaded plane array: keep it instead of re-joining the two stored maps
         self.reuse_planes = reuse_planes
         self._last_planes = {}                              # view -> (H, W, 4) planes of its last pass
-        self._dev_state = {}                                # view -> (planes, costs) DeviceBuffers of its last pass
+        self._dev_state = {}                                # view -> [planes, costs DeviceBuffers, (H, W) held]
         self.exchange = exchange or LocalExchange()
         self.world, self.rank = self.exchange.world, self.exchange.rank
         if self.world > 1 and order == "reference":
@@ -393,7 +393,7 @@ class Pipeline:
             self.image_cache.close()
             self.image_cache = None
         for dev in self._dev_state.values():
-            for b in dev:
+            for b in dev[:2]:
                 b.free()
         self._dev_state = {}
 
@@ -612,15 +612,21 @@ class Pipeline:
         return planes, costs
 
     def _state_buffers(self, ref, shape):
-        """The HBM copy of view `ref`'s last planes and costs (allocated once per view and size)."""
+        """The HBM copy of view `ref`'s last planes and costs: one allocation per view, sized for its
+        full-resolution image (every scale fits, so no free -- a device-wide synchronisation -- between
+        scales)."""
+        need = int(shape[0]) * int(shape[1])
         dev = self._dev_state.get(ref)
-        if dev is None or dev[1].shape != tuple(shape):
+        if dev is None or dev[1].shape[0] < need:
             if dev is not None:
-                for b in dev:
+                for b in dev[:2]:
                     b.free()
-            dev = (capi.DeviceBuffer(self.store.device, (*shape, 4)), capi.DeviceBuffer(self.store.device, shape))
+            full = self.ds.images[ref].shape
+            cap = max(need, int(full[0]) * int(full[1]))
+            dev = [capi.DeviceBuffer(self.store.device, (cap * 4,)), capi.DeviceBuffer(self.store.device, (cap,)), None]
             self._dev_state[ref] = dev
-        return dev
+        dev[2] = tuple(shape)
+        return dev[0], dev[1]
 
     def _upload(self, e, p, images, cams, ids, ref, geom, hier, H, W):
         """InuputInitialization + the state reloads of ProcessProblem (ACMMP.cpp:567-679, 772-843)."""
@@ -635,9 +641,9 @@ class Pipeline:
                 e.upload_depths([self.store.get(key, v) for v in ids])
             planes = self._last_planes.get(ref) if self.reuse_planes else None
             dev = self._dev_state.get(ref)
-            if (planes is not None and planes.shape[:2] == (H, W) and dev is not None and dev[1].shape == (H, W)
+            if (planes is not None and planes.shape[:2] == (H, W) and dev is not None and dev[2] == (H, W)
                     and hasattr(e, "set_state_device")):
-                e.set_state_device(*dev)
+                e.set_state_device(dev[0], dev[1])
                 return
             costs = self.store.get("costs", ref)
             if planes is None or planes.shape[:2] != (H, W):

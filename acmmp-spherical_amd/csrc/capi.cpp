@@ -653,7 +653,11 @@ static acmmp_status upload_depths(acmmp_ctx* c, int n, const float* const* depth
     }
     HIP_TRY(c, dreserve(c->d_dep, c->dep_cap, total));
     for (int i = 0; i < c->N; ++i) {
-        HIP_TRY(c, hipMemcpyAsync(c->d_dep + off[i], depths[i], sizeof(float) * w[i] * h[i], kind, c->stream));
+        // device sources through the copy kernel (compute queue, HBM rate), host ones through the DMA engine
+        if (kind == hipMemcpyDeviceToDevice)
+            HIP_TRY(c, launch_copy(depths[i], c->d_dep + off[i], sizeof(float) * w[i] * h[i], c->stream));
+        else
+            HIP_TRY(c, hipMemcpyAsync(c->d_dep + off[i], depths[i], sizeof(float) * w[i] * h[i], kind, c->stream));
         c->dcams[i].dep_off = static_cast<long long>(off[i]);
         c->dcams[i].dep_w = w[i];
         c->dcams[i].dep_h = h[i];
@@ -701,9 +705,9 @@ acmmp_status acmmp_export_state(acmmp_ctx* c, float* dev_planes, float* dev_cost
     HIP_TRY(c, hipSetDevice(c->device));
     const size_t P = P_of(c);
     if (dev_planes)
-        HIP_TRY(c, hipMemcpyAsync(dev_planes, c->d_planes_rm, sizeof(float4) * P, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(c, launch_copy(c->d_planes_rm, dev_planes, sizeof(float4) * P, c->stream));
     if (dev_costs)
-        HIP_TRY(c, hipMemcpyAsync(dev_costs, c->d_costs_rm, sizeof(float) * P, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(c, launch_copy(c->d_costs_rm, dev_costs, sizeof(float) * P, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));           // another context may read the buffers next
     return ACMMP_OK;
 }
@@ -714,9 +718,9 @@ acmmp_status acmmp_set_state_device(acmmp_ctx* c, const float* dev_planes, const
     HIP_TRY(c, hipSetDevice(c->device));
     const size_t P = P_of(c);
     if (dev_planes)
-        HIP_TRY(c, hipMemcpyAsync(c->d_planes_rm, dev_planes, sizeof(float4) * P, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(c, launch_copy(dev_planes, c->d_planes_rm, sizeof(float4) * P, c->stream));
     if (dev_costs)
-        HIP_TRY(c, hipMemcpyAsync(c->d_costs_rm, dev_costs, sizeof(float) * P, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(c, launch_copy(dev_costs, c->d_costs_rm, sizeof(float) * P, c->stream));
     // stream-ordered before this context's next kernels; the caller keeps the buffers until its run
     return ACMMP_OK;
 }

@@ -182,6 +182,7 @@ hipError_t launch_fuse(int model, const DevCam* cams, const FuseView* views, int
 hipError_t launch_fuse_compact(int W, int H, const float* out_dense, const int* flags, const int* block_offsets,
                                float* out, hipStream_t s);
 hipError_t launch_export_depth(const float4* planes, long long P, float* dst, hipStream_t s);
+hipError_t launch_copy(const void* src, void* dst, size_t bytes, hipStream_t s);  // bytes % 4 == 0
 hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int sw, int sh, int imagescale,
                       float* out, hipStream_t s);
 hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,

@@ -30,9 +30,6 @@
 #define ACMMP_TU -1
 #endif
 #define ACMMP_IN_TU(n) (ACMMP_TU < 0 || ACMMP_TU == (n))
-#ifndef ACMMP_REF_INTERP
-#define ACMMP_REF_INTERP 0
-#endif
 
 namespace acmmp {
 
@@ -1915,7 +1912,7 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
 
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
 template <int MODEL, int VB, bool GEOM, int TF>
-__global__ __launch_bounds__(256, (ACMMP_REF_INTERP && MODEL == kSphere && TF == 2) ? 5 : 1) void k_eval_ref(const KParams kp, const int colour) {
+__global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
@@ -1932,7 +1929,7 @@ __global__ __launch_bounds__(256, (ACMMP_REF_INTERP && MODEL == kSphere && TF ==
         vw = st.vw;
         weight_norm = st.weight_norm;
     }
-    constexpr int kStaged = (MODEL == kSphere && VB <= 4) ? ((ACMMP_REF_INTERP && TF == 2) ? 3 : 4) : 3;
+    constexpr int kStaged = (MODEL == kSphere && VB <= 4) ? 4 : 3;
     Patch pt;
     if constexpr (kStaged == 4) pt = coop_patch_sep<kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
     else pt = coop_patch_nb<MODEL, kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
@@ -2408,8 +2405,8 @@ hipError_t launch_select(const KParams& kp, int colour, int iter, hipStream_t s)
 #if ACMMP_IN_TU(4)
 hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s) {
     const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
-    const bool sep = kp.model == kSphere && pick_vb(kp.V) <= 4 && !(ACMMP_REF_INTERP && tf_of(kp) == 2);
-    const size_t lds_ref = sep ? sep_lds_bytes(kp.S, kp.nside, kRefPix) : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
+    const size_t lds_ref = (kp.model == kSphere && pick_vb(kp.V) <= 4) ? sep_lds_bytes(kp.S, kp.nside, kRefPix)
+                                                                       : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
     hipError_t e = hipSuccess;
     if (kp.ref_split > 0 && (e = hipMemsetAsync(kp.surv_count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
     const dim3 grd_ref = static_cast<unsigned>(cdiv(npix, kRefPix));
@@ -2676,6 +2673,30 @@ hipError_t launch_fuse_compact(int W, int H, const float* out_dense, const int* 
                                float* out, hipStream_t s) {
     const long long P = static_cast<long long>(W) * H;
     k_fuse_scatter<<<static_cast<unsigned>((P + 255) / 256), 256, 0, s>>>(out_dense, flags, P, block_offsets, out);
+    return hipGetLastError();
+}
+
+// A plain copy of n 16-byte words on the compute queue (the state export / restart of a geom pass: at HBM
+// rate, where a device-to-device hipMemcpyAsync of the same 38 MB measured ~9 ms inside the pipeline's
+// overlapped passes)
+__global__ void k_copy16(const uint4* __restrict__ src, long long n, uint4* __restrict__ dst) {
+    for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<long long>(gridDim.x) * blockDim.x)
+        dst[i] = src[i];
+}
+__global__ void k_copy4(const uint32_t* __restrict__ src, long long n, uint32_t* __restrict__ dst) {
+    for (long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<long long>(gridDim.x) * blockDim.x)
+        dst[i] = src[i];
+}
+
+hipError_t launch_copy(const void* src, void* dst, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    const bool wide = bytes % 16 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0 && reinterpret_cast<uintptr_t>(dst) % 16 == 0;
+    const long long n = static_cast<long long>(wide ? bytes / 16 : bytes / 4);
+    const unsigned grd = static_cast<unsigned>(std::min<long long>((n + 255) / 256, 8192));
+    if (wide) k_copy16<<<grd, 256, 0, s>>>(static_cast<const uint4*>(src), n, static_cast<uint4*>(dst));
+    else k_copy4<<<grd, 256, 0, s>>>(static_cast<const uint32_t*>(src), n, static_cast<uint32_t*>(dst));
     return hipGetLastError();
 }
 
