@@ -722,6 +722,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 // one patch column's six samples from its four row nodes (x, y): the bilinear tap and the
                 // sums of ACMMP.cu:488-498
                 auto column = [&](int ci, const float (&nx)[4], const float (&ny)[4]) {
+                    asm volatile("" ::: "memory");
 #pragma unroll
                     for (int cj = 0; cj < 6; ++cj) {
                         float x, y;
@@ -741,7 +742,12 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         y = __builtin_amdgcn_fmed3f(y, 0.0f, c.Hm1f);
                         const Tap t = fetch_tap<TEX, true>(rs, c, x, y);
                         const f32x2 wwr = (f32x2){w, w * r};
-                        ACMMP_ACCUMULATE_T(v, t, w, wwr, r, true);
+                        // unguarded: the view loop skips absent views (`has` re-read per sample kept the
+                        // sums behind a scalar select, 3 v_cndmask per view-sample)
+                        const float sp = lerp_tap<TEX>(t);
+                        ssrs[v] = pk_fma(wwr, splat2(sp), ssrs[v]);
+                        const float ws = w * sp;
+                        sss[v] = fmaf(ws, sp, sss[v]);
                     }
                 };
                 // the view's 16 nodes first -- independent projections the scheduler interleaves (r03 A/B
@@ -769,6 +775,9 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         ny[a][b] = y;
                     }
                 }
+                // the samples re-read (w, r) from LDS rather than keep the nodes' reads live across the
+                // projections (merged, they spilled 210 VGPRs)
+                asm volatile("" ::: "memory");
 #pragma unroll
                 for (int a = 0; a < 4; ++a) column(kNode[a], nx[a], ny[a]);
                 // the interpolated columns 1 and 4 at the node rows, formed after the node columns (fewer
