@@ -27,11 +27,11 @@ EXPORTS = [
     "acmmp_set_scaled_state", "acmmp_set_planar_prior", "acmmp_run_patchmatch", "acmmp_run_patchmatch_ex",
     "acmmp_download", "acmmp_download_aux", "acmmp_device_outputs", "acmmp_synchronize", "acmmp_last_timing",
     "acmmp_last_kernel_timing", "acmmp_last_work", "acmmp_texel_bytes", "acmmp_set_math", "acmmp_get_math", "acmmp_jbu",
-    "acmmp_debug_ncc", "acmmp_debug_geom",
+    "acmmp_debug_ncc", "acmmp_debug_geom", "acmmp_debug_ncc_nb",
     "acmmp_support_points", "acmmp_delaunay", "acmmp_prior_plane_params", "acmmp_depth_from_plane_param",
     "acmmp_planar_prior_host", "acmmp_set_planar_prior_from_maps", "acmmp_download_planar_prior",
     "acmmp_upload_depths_device", "acmmp_upload_views_device", "acmmp_export_depth", "acmmp_export_state", "acmmp_set_state_device", "acmmp_device_alloc", "acmmp_device_free", "acmmp_memcpy",
-    "acmmp_comm_unique_id", "acmmp_comm_create", "acmmp_comm_destroy", "acmmp_comm_broadcast",
+    "acmmp_comm_unique_id", "acmmp_comm_create", "acmmp_comm_destroy", "acmmp_comm_broadcast", "acmmp_comm_after",
     "acmmp_comm_allreduce_max", "acmmp_comm_band_exchange", "acmmp_run_patchmatch_band",
     "acmmp_band_begin", "acmmp_band_sweep", "acmmp_band_sweeps_left", "acmmp_band_halo_ranges",
     "acmmp_band_copy_rows", "acmmp_band_end",
@@ -88,6 +88,7 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_jbu.argtypes = [vp, vp, i32, i32, vp, i32, i32, i32, vp]
     L.acmmp_debug_ncc.argtypes = [vp, i32, vp, vp, vp, vp]
     L.acmmp_debug_geom.argtypes = [vp, i32, vp, vp, vp, vp]
+    L.acmmp_debug_ncc_nb.argtypes = [vp, i32, vp, vp, vp, vp]
     L.acmmp_support_points.argtypes = [vp, i32, i32, vp, i32, vp]
     L.acmmp_delaunay.argtypes = [vp, i32, i32, i32, vp, i32, vp]
     L.acmmp_prior_plane_params.argtypes = [vp, vp, i32, i32, vp, vp]
@@ -104,6 +105,7 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_comm_create.argtypes = [i32, vp, i32, i32, C.POINTER(vp)]
     L.acmmp_comm_destroy.argtypes = [vp]
     L.acmmp_comm_broadcast.argtypes = [vp, i32, vp, vp, vp]
+    L.acmmp_comm_after.argtypes = [vp, vp]
     L.acmmp_comm_allreduce_max.argtypes = [vp, vp, i32]
     L.acmmp_comm_band_exchange.argtypes = [vp, vp, i32, i32, i32]
     L.acmmp_run_patchmatch_band.argtypes = [vp, vp, u64, i32, i32, i32, i32]
@@ -480,6 +482,16 @@ class Context:
     def debug_geom(self, px, py, planes):
         return self._debug(self.L.acmmp_debug_geom, px, py, planes)
 
+    def debug_ncc_nb(self, px, py, planes):
+        """k_eval_nb's own NCC (fast SPHERE >= 1600x800: interpolated coordinates) of planes (n, 8, 4) at
+        pixels (px, py) -> costs (n, 8, V)."""
+        px = np.ascontiguousarray(px, np.int32)
+        py = np.ascontiguousarray(py, np.int32)
+        pl = np.ascontiguousarray(planes, np.float32).reshape(len(px), 8, 4)
+        out = np.empty((len(px), 8, self.N - 1), np.float32)
+        self._check(self.L.acmmp_debug_ncc_nb(self.h, len(px), _p(px), _p(py), _p(pl), _p(out)), "debug_ncc_nb")
+        return out
+
 
 # ---- planar-prior host side (no GPU): ACMMP.cpp:904-1011, main.cpp:113-181 ------------------
 
@@ -612,6 +624,10 @@ class Comm:
         nb = np.array([b.nbytes for b in bufs], np.uint64)
         rt = np.array(roots, np.int32)
         _host_check(self.L.acmmp_comm_broadcast(self.h, n, C.cast(ptrs, C.c_void_p), _p(nb), _p(rt)), "broadcast")
+
+    def after(self, ctx: "Context"):
+        """Collectives queued from now on start after the work `ctx` has queued so far (device-side order)."""
+        _host_check(self.L.acmmp_comm_after(self.h, ctx.h), "comm_after")
 
     def band_exchange(self, ctx: "Context", colour: int, rank_up: int, rank_down: int):
         _host_check(self.L.acmmp_comm_band_exchange(self.h, ctx.h, colour, rank_up, rank_down), "band_exchange")

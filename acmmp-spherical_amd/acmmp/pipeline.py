@@ -253,6 +253,9 @@ class RcclExchange:
 
     def share(self, key, views, owners, store):
         bufs = [store.device_map(key, v) for v in views]
+        # the broadcast reads maps the engine contexts exported on their own streams: order it after them
+        for ctx in store.take_producers():
+            self.comm.after(ctx)
         self.comm.broadcast(bufs, [owners[v] for v in views])
         for v in views:
             if owners[v] != self.rank:
@@ -270,6 +273,11 @@ class ViewStore:
         self.host = {}                               # (key, view) -> np.ndarray
         self.dev = {}                                # (key, view) -> capi.DeviceBuffer
         self.shapes = {}                             # (key, view) -> (H, W)
+        self.producers = []                          # contexts that exported maps since the last exchange
+
+    def take_producers(self):
+        p, self.producers = self.producers, []
+        return p
 
     def put(self, key, view, arr, ctx=None):
         # float32 views are kept as they are (a depth or normals slice of the downloaded planes costs no
@@ -281,6 +289,8 @@ class ViewStore:
             buf = self.device_map(key, view, arr.shape)
             if ctx is not None and hasattr(ctx, "export_depth"):
                 ctx.export_depth(buf)                # HBM -> HBM, no host round trip
+                if all(c is not ctx for c in self.producers):
+                    self.producers.append(ctx)
             else:
                 buf.upload(arr)
 
@@ -365,9 +375,29 @@ class Pipeline:
         self._math = math
         # prepared (padded + binary16) images of every (view, scale), shared by this pipeline's contexts:
         # each is prepared once, not once per problem that reads it
-        self.image_cache = capi.ImageCache(device, int(os.environ.get("ACMMP_IMAGE_CACHE_BYTES", 0))) if gpu else None
+        budget = os.environ.get("ACMMP_IMAGE_CACHE_BYTES")
+        budget = int(budget) if budget is not None else self._default_cache_budget(ds, max(slots, 1))
+        self.image_cache = capi.ImageCache(device, budget) if gpu else None
         if gpu:
             self.log(f"engine math: {self.engine.math()}")
+
+    @staticmethod
+    def _default_cache_budget(ds, contexts):
+        """Soft byte budget of the prepared-image cache: every (view, scale) of a dataset up to 32 GiB stays
+        in HBM for the whole run (no re-preparation between passes); beyond that, 4x the largest problem's
+        full-scale working set per context (the views a problem pins plus room for the next problem's),
+        least recently used entries evicted first.  One prepared view = padded fp32 + binary16 copy."""
+        def view_bytes(v):
+            im = ds.images[v]
+            h, w = im.shape[:2]
+            return 6 * (w + 2) * (h + 2)
+        views = list(ds.images)
+        total = sum(view_bytes(v) for v in views) * 4 // 3           # + the coarser scales
+        if total <= 32 << 30:
+            return 0
+        largest = max((view_bytes(p.ref_image_id) + sum(view_bytes(s) for s in p.src_image_ids)
+                       for p in ds.problems if p.ref_image_id in ds.images), default=0)
+        return max(32 << 30, 4 * contexts * largest)
 
     @contextlib.contextmanager
     def _timed(self, stage):
@@ -603,6 +633,9 @@ class Pipeline:
                 # the same planes and costs kept in HBM too: the next geom pass restarts from them device
                 # to device (set_state_device) instead of uploading them from the host again
                 e.export_state(*self._state_buffers(ref, costs.shape))
+            elif ref in self._dev_state:
+                # no HBM copy of these planes: an older one must not pass for them in _upload
+                self._dev_state[ref][2] = None
             if self.out_folder:
                 d = os.path.join(self.out_folder, "ACMMP", f"2333_{ref:08d}")
                 os.makedirs(d, exist_ok=True)

@@ -407,16 +407,18 @@ static void unpin_views(acmmp_ctx* c) {
     cache_release(k);
 }
 
-// Least-recently used unpinned entries go first; the budget is soft (pinned entries stay).
-static void evict_over_budget(acmmp_image_cache* k) {
+// Least-recently used unpinned entries go first; the budget is soft (pinned entries stay).  Called with
+// the cache mutex held: the evicted allocations are handed back in `dead` and freed by the caller after
+// it releases the lock (hipFree waits for the device, which would stall every other context's upload).
+static void evict_over_budget(acmmp_image_cache* k, std::vector<void*>& dead) {
     if (k->budget == 0) return;
     while (k->bytes > k->budget) {
         auto victim = k->map.end();
         for (auto it = k->map.begin(); it != k->map.end(); ++it)
             if (it->second.pins == 0 && (victim == k->map.end() || it->second.used < victim->second.used)) victim = it;
         if (victim == k->map.end()) return;
-        dfree(victim->second.img);
-        dfree(victim->second.img16);
+        dead.push_back(victim->second.img);
+        dead.push_back(victim->second.img16);
         k->bytes -= victim->second.bytes;
         k->map.erase(victim);
         ++k->evictions;
@@ -444,12 +446,15 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));          // the previous problem's kernels read the old images
     unpin_views(c);
+    // until this call succeeds the context holds no usable views: a failure below must not leave N > 0
+    // with camera entries pointing at images that are now unpinned, reallocated or freed
+    c->N = 0;
+    c->tex16 = false;
     const bool resized = (c->W != cams[0].width || c->H != cams[0].height);
     // a new problem: the previous problem's prior / scaled state no longer applies (the reference
     // builds a fresh ACMMP object per ProcessProblem, main.cpp:80)
     c->has_prior = false;
     c->has_scaled = false;
-    c->N = n;
     c->W = cams[0].width;
     c->H = cams[0].height;
     c->model = cams[0].model;
@@ -504,6 +509,17 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
     }
     std::vector<float*> own(n, nullptr);
     std::vector<uint32_t*> own16(n, nullptr);
+    // keyed misses that did not end up in the cache -- all of them when a step below fails -- stay with
+    // this context until its next upload (unpin_views frees them)
+    struct OwnGuard {
+        acmmp_ctx* c;
+        std::vector<float*>& own;
+        std::vector<uint32_t*>& own16;
+        ~OwnGuard() {
+            for (float* p : own) if (p) c->orphans.push_back(p);
+            for (uint32_t* p : own16) if (p) c->orphans16.push_back(p);
+        }
+    } own_guard{c, own, own16};
     for (int i : miss) {
         if (keyed[i]) {
             const size_t texels = static_cast<size_t>(cams[i].width + 2) * (cams[i].height + 2);
@@ -549,43 +565,42 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
         HIP_TRY(c, hipStreamSynchronize(c->stream));      // staging, padding and flags done before returning
         for (int i : miss) {
             if (inexact[i]) {
-                if (keyed[i]) dfree(own16[i]);
+                if (keyed[i]) { dfree(own16[i]); own16[i] = nullptr; }
                 base16[i] = nullptr;
             }
         }
         if (cache && keys) {
-            std::lock_guard<std::mutex> lk(cache->mu);
-            for (int i : miss) {
-                if (!keyed[i]) continue;
-                auto it = cache->map.find(keys[i]);
-                if (it != cache->map.end()) {
-                    if (it->second.pins > 0) {              // another context inserted it meanwhile: use ours privately
-                        keyed[i] = false;
-                        continue;
+            std::vector<void*> dead;
+            {
+                std::lock_guard<std::mutex> lk(cache->mu);
+                for (int i : miss) {
+                    if (!keyed[i]) continue;
+                    auto it = cache->map.find(keys[i]);
+                    if (it != cache->map.end()) {
+                        if (it->second.pins > 0) {              // another context inserted it meanwhile: use ours privately
+                            keyed[i] = false;
+                            continue;
+                        }
+                        dead.push_back(it->second.img);
+                        dead.push_back(it->second.img16);
+                        cache->bytes -= it->second.bytes;
+                        cache->map.erase(it);
                     }
-                    dfree(it->second.img);
-                    dfree(it->second.img16);
-                    cache->bytes -= it->second.bytes;
-                    cache->map.erase(it);
-                }
-                acmmp_image_cache::Entry e;
-                e.W = cams[i].width; e.H = cams[i].height;
-                e.img = own[i]; e.img16 = own16[i];
-                e.f16_checked = want16;
-                e.bytes = sizeof(float) * static_cast<size_t>(e.W + 2) * (e.H + 2) * (own16[i] ? 2 : 1);
-                e.pins = 1;
-                e.used = ++cache->clock;
-                cache->bytes += e.bytes;
-                cache->map.emplace(keys[i], e);
-                c->pinned.push_back(keys[i]);
-                own[i] = nullptr; own16[i] = nullptr;      // owned by the cache now
+                    acmmp_image_cache::Entry e;
+                    e.W = cams[i].width; e.H = cams[i].height;
+                    e.img = own[i]; e.img16 = own16[i];
+                    e.f16_checked = want16;
+                    e.bytes = sizeof(float) * static_cast<size_t>(e.W + 2) * (e.H + 2) * (own16[i] ? 2 : 1);
+                    e.pins = 1;
+                    e.used = ++cache->clock;
+                    cache->bytes += e.bytes;
+                    cache->map.emplace(keys[i], e);
+                    c->pinned.push_back(keys[i]);
+                    own[i] = nullptr; own16[i] = nullptr;      // owned by the cache now
             }
-            evict_over_budget(cache);
-        }
-        // keyed misses that could not enter the cache stay with this context until its next upload
-        for (int i : miss) {
-            if (own[i]) c->orphans.push_back(own[i]);
-            if (own16[i]) c->orphans16.push_back(own16[i]);
+            evict_over_budget(cache, dead);
+            }
+            for (void* p : dead) dfree(p);
         }
     }
     c->tex16 = want16;
@@ -635,6 +650,7 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
     // another view's costs into k_finish's hierarchy gate
     HIP_TRY(c, hipMemsetAsync(c->d_pre, 0, sizeof(float) * P_of(c), c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->N = n;
     return ACMMP_OK;
 }
 
@@ -861,11 +877,13 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.model = c->model;
     kp.W = c->W; kp.H = c->H; kp.Wh = Wh_of(c); kp.N = c->N; kp.V = c->N - 1;
     kp.R = R; kp.inc = p.radius_increment; kp.nside = nside; kp.S = nside * nside;
-    // interpolated SPHERE sample coordinates in the fast k_eval_nb: 6x6 patches, and
-    // reference pixels of at most 2 pi / 1600 rad -- below that the patch's angular span makes the
-    // interpolation's float64 NCC error exceed 1e-4 in the tail (scripts/interp_feasibility.py; at
-    // 1600x800 the largest error is 6.7e-5, at 1280x640 8.5e-3)
-    kp.interp = c->model == kSphere && nside == 6 && c->W >= 1600 && c->H >= 800;
+    // interpolated SPHERE sample coordinates in the fast k_eval_nb: 6x6 patches whose
+    // radius spans at most 5 pixels of 2 pi / 1600 rad (the geometry the float64 study validated:
+    // patch_size 11, radius_increment 2 from 1600x800 up) -- a wider patch angle makes the interpolation's
+    // NCC error exceed 1e-4 in the tail (scripts/interp_feasibility.py; at 1600x800 the largest error is
+    // 6.7e-5, at 1280x640, R = 5 spanning 1.25x the angle, 8.5e-3).  patch_size 21 / increment 4 also
+    // gives 6x6 samples but spans twice the angle: it projects every sample below 3200x1600.
+    kp.interp = c->model == kSphere && nside == 6 && 1600LL * R <= 5LL * c->W && 800LL * R <= 5LL * c->H;
     kp.rows = std::min(c->H, 32 * (((c->H / 2) + 15) / 16));
     kp.row_lo = 0; kp.row_hi = kp.rows;
     kp.init_lo = 0; kp.init_hi = c->H;
@@ -1044,6 +1062,13 @@ void band_ranges(const KParams& kp, int lo, int hi, int& sup_a, int& sup_b, int&
 }
 
 }  // namespace
+
+acmmp_status acmmp::engine_stream(acmmp_ctx* c, int* device, hipStream_t* stream) {
+    if (!c || !device || !stream) return ACMMP_ERR_INVALID_ARGUMENT;
+    *device = c->device;
+    *stream = c->stream;
+    return ACMMP_OK;
+}
 
 acmmp_status acmmp::band_buffers(acmmp_ctx* c, int colour, BandBuffers* b) {
     if (!c || !b || colour < 0 || colour > 1) return ACMMP_ERR_INVALID_ARGUMENT;
@@ -1239,6 +1264,7 @@ acmmp_status acmmp_jbu(acmmp_ctx* c, const float* ref, int W, int H, const float
     return ACMMP_OK;
 }
 
+// which: 0 = NCC (per-sample projection), 1 = geom cost, 2 = k_eval_nb's NCC on n pixels x 8 planes
 static acmmp_status debug_eval(acmmp_ctx* c, int which, int n, const int* px, const int* py, const float* planes,
                                float* out) {
     if (!c || !px || !py || !planes || !out || n <= 0) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "bad debug args");
@@ -1253,15 +1279,18 @@ static acmmp_status debug_eval(acmmp_ctx* c, int which, int n, const int* px, co
     int *dx = nullptr, *dy = nullptr;
     float4* dp = nullptr;
     float* dout = nullptr;
-    const size_t nout = static_cast<size_t>(n) * kp.V;
+    const int per = which == 2 ? 8 : 1;                   // planes per query pixel
+    const size_t nout = static_cast<size_t>(n) * per * kp.V;
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&dx), sizeof(int) * n);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&dy), sizeof(int) * n);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&dp), sizeof(float4) * n);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&dp), sizeof(float4) * n * per);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&dout), sizeof(float) * nout);
     if (e == hipSuccess) e = hipMemcpy(dx, px, sizeof(int) * n, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(dy, py, sizeof(int) * n, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dp, planes, sizeof(float4) * n, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = launch_debug(kp, which, n, dx, dy, dp, dout, c->stream);
+    if (e == hipSuccess) e = hipMemcpy(dp, planes, sizeof(float4) * n * per, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = which == 2 ? launch_debug_nb(kp, n, dx, dy, dp, dout, c->stream)
+                       : launch_debug(kp, which, n, dx, dy, dp, dout, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(float) * nout, hipMemcpyDeviceToHost);
     dfree(dx); dfree(dy); dfree(dp); dfree(dout);
@@ -1274,6 +1303,9 @@ acmmp_status acmmp_debug_ncc(acmmp_ctx* c, int n, const int* px, const int* py, 
 }
 acmmp_status acmmp_debug_geom(acmmp_ctx* c, int n, const int* px, const int* py, const float* planes, float* out) {
     return debug_eval(c, 1, n, px, py, planes, out);
+}
+acmmp_status acmmp_debug_ncc_nb(acmmp_ctx* c, int n, const int* px, const int* py, const float* planes, float* costs) {
+    return debug_eval(c, 2, n, px, py, planes, costs);
 }
 
 }  // extern "C"

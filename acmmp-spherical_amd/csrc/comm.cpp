@@ -24,6 +24,7 @@ struct acmmp_comm {
     hipStream_t stream = nullptr;
     double* d_scratch = nullptr;
     int scratch_n = 0;
+    hipEvent_t after = nullptr;         // acmmp_comm_after: engine-stream work the next collectives wait for
 };
 
 namespace {
@@ -94,8 +95,25 @@ void acmmp_comm_destroy(acmmp_comm* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
     if (c->d_scratch) (void)hipFree(c->d_scratch);
+    if (c->after) (void)hipEventDestroy(c->after);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
+}
+
+acmmp_status acmmp_comm_after(acmmp_comm* c, acmmp_ctx* ctx) {
+    if (!c || !ctx) return ACMMP_ERR_INVALID_ARGUMENT;
+    int dev = 0;
+    hipStream_t s = nullptr;
+    acmmp_status st = acmmp::engine_stream(ctx, &dev, &s);
+    if (st != ACMMP_OK) return st;
+    if (dev != c->device) return ACMMP_ERR_INVALID_ARGUMENT;
+    TRY_HIP(hipSetDevice(c->device));
+    if (!c->after) TRY_HIP(hipEventCreateWithFlags(&c->after, hipEventDisableTiming));
+    // the engine stream's work so far -> an event the communicator's stream waits on: device-side order,
+    // no host wait (a later record re-arms the same event; a wait already queued keeps its snapshot)
+    TRY_HIP(hipEventRecord(c->after, s));
+    TRY_HIP(hipStreamWaitEvent(c->stream, c->after, 0));
+    return ACMMP_OK;
 }
 
 acmmp_status acmmp_comm_broadcast(acmmp_comm* c, int n, void* const* bufs, const size_t* bytes, const int* roots) {

@@ -173,6 +173,8 @@ struct BandBuffers {
     int device;
 };
 acmmp_status band_buffers(acmmp_ctx* c, int colour, BandBuffers* out);
+// The context's device and engine stream (every kernel and copy of the context is queued there).
+acmmp_status engine_stream(acmmp_ctx* c, int* device, hipStream_t* stream);
 
 // SimpleFusionKernel (ACMMP.cu:1662-1814) for reference view `ref` + compaction in pixel order:
 // out_dense/flags are P-sized scratch, block_counts ceil(P/256) ints.
@@ -187,6 +189,9 @@ hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int s
                       float* out, hipStream_t s);
 hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,
                         float* out, hipStream_t s);
+// k_eval_nb's NCC instance on n pixels x 8 planes (planes[q * 8 + h]): out[(q * 8 + h) * V + v]
+hipError_t launch_debug_nb(const KParams& kp, int n, const int* px, const int* py, const float4* planes, float* out,
+                           hipStream_t s);
 // Row-pair binary16 copy of one padded view (W + 2) x (H + 2) (DevCam::img16_base layout); *inexact
 // (device int, pre-zeroed) is set when a texel is not exactly representable as a normal binary16
 // number or zero.

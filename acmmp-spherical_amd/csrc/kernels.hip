@@ -712,6 +712,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             constexpr float kL1[4] = {0.26666667f, 1.3333334f, -0.6666667f, 0.06666667f};
             constexpr float kL4[4] = {0.06666667f, -0.6666667f, 1.3333334f, 0.26666667f};
             constexpr int kNode[4] = {0, 2, 3, 5};
+            constexpr float kSpreadMax = 64.0f;     // source pixels spanned by the corner nodes (see below)
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
                 if (!has(v)) continue;
@@ -775,6 +776,19 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         ny[a][b] = y;
                     }
                 }
+                // The interpolation holds where the source mapping is smooth over the patch.  Where the four
+                // corner nodes spread over more than kSpreadMax source pixels in x or y -- a patch landing
+                // next to a source pole (longitude stretches as 1 / cos(latitude)) or a near-grazing plane
+                // whose depth flips sign inside the patch -- the lane projects all 36 samples instead, in the
+                // per-sample loop's order and arithmetic (so those costs are the per-sample fast ones bit for
+                // bit).  float64 study (tests/np_interp.py, tests/test_interp_design.py): with the test, the
+                // interpolated NCC stays within 4e-5 of the projected one on every query tried from 1600x800
+                // up, pole-adjacent and random planes included; without it the tail reached 0.6.
+                const float sx_ = fmaxf(fmaxf(nx[0][3], nx[3][0]), fmaxf(nx[3][3], 0.0f)) -
+                                  fminf(fminf(nx[0][3], nx[3][0]), fminf(nx[3][3], 0.0f));
+                const float sy_ = fmaxf(fmaxf(ny[0][0], ny[0][3]), fmaxf(ny[3][0], ny[3][3])) -
+                                  fminf(fminf(ny[0][0], ny[0][3]), fminf(ny[3][0], ny[3][3]));
+                const bool smooth = fmaxf(sx_, sy_) <= kSpreadMax;
                 // the samples re-read (w, r) from LDS rather than keep the nodes' reads live across the
                 // projections (merged, they spilled 210 VGPRs)
                 asm volatile("" ::: "memory");
@@ -796,6 +810,31 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 }
                 column(1, c1x, c1y);
                 column(4, c4x, c4y);
+                // lanes whose corners spread too far redo the view with every sample projected (the
+                // !interp_done loop's arithmetic and order), after the interpolated pass so that no node
+                // stays live across the branch (as an if / else around the columns: 259 VGPRs spilled)
+                if (!smooth) {
+                    ssrs[v] = splat2(0.f);
+                    sss[v] = 0.f;
+#pragma nounroll
+                    for (int s = 0; s < 36; ++s) {
+                        const int jj = s - (s / 6) * 6;
+                        const float4 q = pt.rw[s * pt.stride];
+                        const float4 rw = make_float4(q.x, pt.rr[jj * pt.stride], q.y, q.z);
+                        const float dep = depth_from_plane_fast(ph, rw);
+                        float x, y;
+                        project_fast<MODEL>(c, cam_point_fast<MODEL>(c, 0, 0, dep, rw), x, y);
+                        x = fmaf(-floorf(x * c.invW), c.Wf, x);
+                        y = __builtin_amdgcn_fmed3f(y, 0.0f, c.Hm1f);
+                        const Tap t = fetch_tap<TEX, true>(rs, c, x, y);
+                        const float w = rw.w, r = q.w;
+                        const f32x2 wwr = (f32x2){w, w * r};
+                        const float sp = lerp_tap<TEX>(t);
+                        ssrs[v] = pk_fma(wwr, splat2(sp), ssrs[v]);
+                        const float ws = w * sp;
+                        sss[v] = fmaf(ws, sp, sss[v]);
+                    }
+                }
                 __builtin_amdgcn_sched_barrier(0);           // one view's nodes live at a time
             }
         }
@@ -2385,6 +2424,45 @@ hipError_t launch_eval_nb(const KParams& kp0, int colour, hipStream_t s) {
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// Test hook (acmmp_debug_ncc_nb): k_eval_nb's NCC code on given queries of one pixel and 8 planes (the 8
+// neighbour hypotheses of k_eval_nb) -- the same coop_patch_nb staging and the same for_all_views_t
+// instance (view chunk, STAGED 3, PIPE, TEX, FM), so in the fast SPHERE mode of views >= 1600x800 the
+// interpolated source coordinates of DESIGN.md §2.4, which acmmp_debug_ncc (per-sample projection) does
+// not run.  out[(q * 8 + h) * V + v].
+template <int MODEL, int VB, int TEX, int FM>
+__global__ __launch_bounds__(256) void k_debug_nb(const KParams kp, int n, const int* __restrict__ qx,
+                                                  const int* __restrict__ qy, const float4* __restrict__ planes,
+                                                  float* __restrict__ out) {
+    extern __shared__ float4 lds4[];
+    const int t = threadIdx.x;
+    const int lp = t / kNbLanes, h = t - lp * kNbLanes;
+    const int q = blockIdx.x * kNbPix + lp;
+    const bool valid = q < n;
+    const int px = valid ? qx[q] : 0, py = valid ? qy[q] : 0;
+    const Patch pt = coop_patch_nb<MODEL>(kp, valid, px, py, lp, h, lds4);
+    if (!valid) return;
+    const long long k = static_cast<long long>(q) * kNbLanes + h;
+    const float4 ph = planes[k];
+    float* o = out + k * kp.V;
+    const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
+    for_all_views_t<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
+        kp, px, py, pt, ph, all, [&](int v, float c) { o[v] = c; });
+}
+
+hipError_t launch_debug_nb(const KParams& kp, int n, const int* px, const int* py, const float4* planes, float* out,
+                           hipStream_t s) {
+    const size_t lds_nb = nb_lds_bytes(kp.model, kp.S, kp.nside);
+    const dim3 grd = static_cast<unsigned>(cdiv(n, kNbPix));
+    if (kp.fast) {
+        if (kp.tex16) ACMMP_DISPATCH(kp.model, kp.V, (k_debug_nb<M, VBC, 1, 1><<<grd, 256, lds_nb, s>>>(kp, n, px, py, planes, out)));
+        else ACMMP_DISPATCH(kp.model, kp.V, (k_debug_nb<M, VBC, 0, 1><<<grd, 256, lds_nb, s>>>(kp, n, px, py, planes, out)));
+    } else {
+        if (kp.tex16) ACMMP_DISPATCH(kp.model, kp.V, (k_debug_nb<M, VBC, 1, 0><<<grd, 256, lds_nb, s>>>(kp, n, px, py, planes, out)));
+        else ACMMP_DISPATCH(kp.model, kp.V, (k_debug_nb<M, VBC, 0, 0><<<grd, 256, lds_nb, s>>>(kp, n, px, py, planes, out)));
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_eval_nb_views(const KParams& kp, int colour, hipStream_t s) {

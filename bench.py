@@ -56,6 +56,26 @@ def eval_nb_flop_per_pixel(model: str, V: int, samples: int = 36) -> float:
     return 8 * samples * (V * F_HVS[model] + 15.0) + samples * 30.0
 
 
+# What the fast SPHERE k_eval_nb executes per hypothesis and view when it interpolates (DESIGN.md §2.4,
+# capi.cpp build_kparams' gate): 16 node samples projected in full (ray-plane depth and camera point 15 +
+# F_HVS 100 each), the 20 other samples' bilinear fetch + accumulation (19 of F_HVS: SURVEY.md §8d's pinhole
+# breakdown) on interpolated coordinates, and the interpolation itself: node unwrap 15 x 5, the 8 Lagrange
+# samples of the node columns 8 x 14, columns 1 / 4 at the node rows 16 x 8, their 4 other samples 4 x 14,
+# and the 20 samples' seam wrap and clamp 20 x 6 -- 491 FLOP.  Per pixel the 8 hypotheses plus the 36 shared
+# bilateral weights.
+F_INTERP_VIEW = 16 * (100.0 + 15.0) + 20 * 19.0 + 491.0
+
+
+def eval_nb_executed_flop_per_pixel(V: int) -> float:
+    return 8 * V * F_INTERP_VIEW + 36 * 30.0
+
+
+def interp_enabled(width: int, height: int, patch_size: int = 11, radius_increment: int = 2) -> bool:
+    """capi.cpp build_kparams' gate (tests/np_interp.interp_enabled)."""
+    R = patch_size // 2
+    return len(range(-R, R + 1, radius_increment)) == 6 and 1600 * R <= 5 * width and 800 * R <= 5 * height
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -248,6 +268,19 @@ def guarded(fn, seconds, *a):
     return box["r"], False
 
 
+EXIT_ABANDONED = 3
+
+
+def leave_abandoned():
+    """A multi-rank extra was abandoned at its deadline and a worker thread may still be blocked inside a
+    collective: leave without tearing down the process group or the context it uses, and with a non-zero
+    status, so a hung first RCCL run never reads as success (the headline line is already out; every rank
+    reaches this at the same deadline)."""
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(EXIT_ABANDONED)
+
+
 def depth_exchange(args, ctx, rank, world, device, dist, allmax, reps=5):
     """Every rank broadcasts its last depth map (W x H float32, acmmp_export_depth: HBM to HBM) to all
     ranks in one grouped RCCL call -- what pipeline.RcclExchange does between two passes.  The RCCL
@@ -259,6 +292,7 @@ def depth_exchange(args, ctx, rank, world, device, dist, allmax, reps=5):
         comm = capi.Comm(device, uid[0], world, rank)
         bufs = [capi.DeviceBuffer(device, (args.height, args.width)) for _ in range(world)]
         ctx.export_depth(bufs[rank])
+        comm.after(ctx)                                              # the broadcast waits for the export
         comm.broadcast(bufs, list(range(world)))                     # warm-up
         ok = all(np.isfinite(b.download()).mean() > 0.5 for b in bufs)
         dist.barrier()
@@ -402,14 +436,27 @@ def pipeline_mode(args, rank, world, local_rank, barrier, allmax):
 
 
 def visible_gpus() -> int:
-    """GPUs this process could use, counted without initialising a HIP runtime in it (torch's
-    device_count does not initialise the device on this image; the launcher parent never touches a
-    GPU, so it may start its children with no HIP state to inherit)."""
+    """GPUs this process could use, counted without any HIP call: the KFD topology's GPU nodes (a node
+    with a non-zero gfx_target_version; CPU nodes report 0), limited by the visibility variables the HIP
+    runtime honours.  The launcher parent must stay free of HIP state, since it starts the ranks."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
     try:
-        import torch
-        return int(torch.cuda.device_count())
-    except Exception:                                                # noqa: BLE001
+        for node in sorted(os.listdir(root)):
+            try:
+                with open(os.path.join(root, node, "properties")) as fh:
+                    props = dict(ln.split(None, 1) for ln in fh if len(ln.split(None, 1)) == 2)
+            except OSError:
+                continue
+            if int(props.get("gfx_target_version", "0").strip() or 0) != 0:
+                n += 1
+    except OSError:
         return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([t for t in v.split(",") if t.strip() != ""]))
+    return n
 
 
 def launch_ranks(args) -> int:
@@ -460,9 +507,16 @@ def dry_run(args, rank, world, dist):
         pids = sorted({g["pid"] for g in got})
     else:
         pids = [os.getpid()]
+    # ACMMP_BENCH_SELFTEST_ABANDON=1: a guarded extra that hangs past its deadline, left through the same
+    # exit path as main()'s (tests/test_bench_launch.py)
+    selftest = os.environ.get("ACMMP_BENCH_SELFTEST_ABANDON") == "1"
+    extra, abandoned = guarded(time.sleep, 0.5, 30) if selftest else (None, False)
     if rank == 0:
         print(json.dumps({"dry_run": True, "ranks": world, "rank_ids": ranks, "processes": len(pids),
-                          "backend": dist.get_backend() if dist is not None else None, "gpus": args.gpus}), flush=True)
+                          "backend": dist.get_backend() if dist is not None else None, "gpus": args.gpus,
+                          "extra": extra}), flush=True)
+    if abandoned:
+        leave_abandoned()
     if dist is not None:
         dist.destroy_process_group()
 
@@ -537,13 +591,25 @@ def main():
         ctx.synchronize()
         barrier()
         t_o = time.perf_counter()
+        o_nb = [0.0, 0, 0]
         for k in range(args.steps):
             ctx.run_patchmatch(args.seed + k)
+            ms, n = ctx.last_kernel_timing()["k_eval_nb"]
+            o_nb[0] += ms
+            o_nb[1] += n
+            o_nb[2] += ctx.last_work()[0]
         ctx.synchronize()
         barrier()
         el_o = allmax(time.perf_counter() - t_o)
+        o_launch = o_nb[0] / max(o_nb[1], 1)
+        o_flop = eval_nb_flop_per_pixel(args.model, args.n_src) * o_nb[2] / max(o_nb[1], 1)
+        o_tf = o_flop / (o_launch * 1e-3) / 1e12
         other = {"math": om, "value": round(args.width * args.height * args.iters * args.steps * world / el_o / 1e6, 3),
                  "ms_per_step": round(el_o / args.steps * 1e3, 3),
+                 "roofline": {"kernel": "k_eval_nb", "bound": "valu", "launch_ms": round(o_launch, 4),
+                              "launches": o_nb[1], "flop_per_launch": o_flop, "achieved": round(o_tf, 3),
+                              "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(o_tf / PEAK_FP32_TFLOPS, 4),
+                              "note": "every sample projected in this mode: algorithmic = executed"},
                  "note": "exact = bit-identical to the CPU oracle; fast = tolerance parity (DESIGN.md §2.4)"}
         ctx.set_math(args.math)
 
@@ -602,6 +668,14 @@ def main():
                            "frac": round(gbs / PEAK_HBM_GBS, 4), "source": os.path.relpath(args.pmc, REPO)}
         except (OSError, ValueError, AttributeError):
             pass
+    # the fast SPHERE instance projects 16 of the 36 samples per hypothesis and view and interpolates the
+    # rest: `frac` prices the algorithmic work it replaces, `executed` what it performs
+    executed = None
+    if args.math == "fast" and args.model == "sphere" and interp_enabled(args.width, args.height):
+        ex_flop = eval_nb_executed_flop_per_pixel(args.n_src) * pix_per_launch
+        ex_tf = ex_flop / (launch_ms * 1e-3) / 1e12
+        executed = {"flop_per_launch": ex_flop, "achieved": round(ex_tf, 3), "frac": round(ex_tf / PEAK_FP32_TFLOPS, 4),
+                    "note": "16 projected + 20 interpolated samples per hypothesis-view (bench.F_INTERP_VIEW)"}
     roofline = {
         "bound": "valu",
         "achieved": round(achieved, 3),
@@ -616,6 +690,7 @@ def main():
         "evaluated_pixels_per_launch": round(pix_per_launch),
         "short_circuited_pixel_frac": round(1.0 - work[0] / max(work[1], 1), 4),
         "hbm": hbm,
+        "executed": executed,
         "half_sweep_kernels_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items()},
         "half_sweep_reference_flop_tflops": round(algorithmic_flop_per_pixel(args.model, args.n_src) *
                                                   pix_per_launch / (sum(v[0] for v in kern.values()) /
@@ -688,11 +763,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if abandoned:
-        # a worker thread is blocked inside a collective: leave without tearing down the process group or
-        # the context it uses (the headline line is out; every rank reaches this at the same deadline)
-        sys.stdout.flush()
-        sys.stderr.flush()
-        os._exit(0)
+        leave_abandoned()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -259,6 +259,12 @@ acmmp_status acmmp_comm_create(int device, const uint8_t id[ACMMP_COMM_ID_BYTES]
                                acmmp_comm **out);
 void acmmp_comm_destroy(acmmp_comm *comm);
 
+/* Orders every collective queued on comm after this call behind all the work ctx (a context of the
+ * same GPU) has queued so far -- e.g. acmmp_export_depth into a buffer about to be broadcast: an event
+ * recorded on the engine stream that the communicator's stream waits on, no host wait.  No reference
+ * counterpart (the reference hands depth maps over through depths*.dmb files, ACMMP.cpp:653-678). */
+acmmp_status acmmp_comm_after(acmmp_comm *comm, acmmp_ctx *ctx);
+
 /* Grouped in-place broadcasts: device buffer bufs[i] (bytes[i]) from rank roots[i] to every rank.
  * Synchronous on return. */
 acmmp_status acmmp_comm_broadcast(acmmp_comm *comm, int n, void *const *bufs, const size_t *bytes,
@@ -346,6 +352,12 @@ acmmp_status acmmp_jbu(acmmp_ctx *ctx, const float *ref, int W, int H, const flo
  * pixel (px[k], py[k]) against source v+1. */
 acmmp_status acmmp_debug_ncc(acmmp_ctx *ctx, int n, const int *px, const int *py, const float *planes,
                              float *costs);
+/* costs[(k*8 + h)*(num_images-1) + v] = ComputeBilateralNCC (ACMMP.cu:405-516) of plane
+ * planes[k*8 + h] at pixel (px[k], py[k]) against source v+1, evaluated by k_eval_nb's own NCC
+ * code (the propagation kernel of CheckerboardPropagation, ACMMP.cu:1146-1233): in the fast math
+ * mode on SPHERE views from 1600x800 up, with its interpolated sample coordinates. */
+acmmp_status acmmp_debug_ncc_nb(acmmp_ctx *ctx, int n, const int *px, const int *py, const float *planes,
+                                float *costs);
 /* out[k*(num_images-1) + v] = ComputeGeomConsistencyCost (ACMMP.cu:646-671). */
 acmmp_status acmmp_debug_geom(acmmp_ctx *ctx, int n, const int *px, const int *py, const float *planes,
                               float *out);

@@ -62,6 +62,32 @@ def test_launcher_world_mismatch_is_an_error():
     assert r.returncode != 0 and "launcher started 1" in r.stderr
 
 
+def test_abandoned_extra_exits_nonzero():
+    """A guarded extra abandoned at its deadline (a hung first RCCL run) prints the line with the error and
+    then exits non-zero on every rank, so the driver does not read the hang as success."""
+    r = _bench("--gpus", "2", "--dry-run", env={"ACMMP_BENCH_SELFTEST_ABANDON": "1"})
+    assert r.returncode != 0, r.stderr[-2000:]
+    line = _json_line(r.stdout)
+    assert line["ranks"] == 2 and "abandoned" in line["extra"]["error"]
+    r1 = _bench("--dry-run", env={"ACMMP_BENCH_SELFTEST_ABANDON": "1"})
+    assert r1.returncode == 3
+
+
+def test_visible_gpus_counts_without_hip():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    n = bench.visible_gpus()
+    assert n >= 0
+    os.environ["HIP_VISIBLE_DEVICES"] = ""
+    try:
+        assert bench.visible_gpus() == 0
+    finally:
+        del os.environ["HIP_VISIBLE_DEVICES"]
+    assert "torch" not in bench.visible_gpus.__code__.co_names
+
+
 def test_multi_rank_extras_are_guarded():
     """The first runs of the RCCL extras (depth_exchange, band_split) cannot cost the headline line: an
     exception is reported in the line, and a hang is abandoned at the deadline."""

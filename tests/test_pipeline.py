@@ -169,6 +169,22 @@ def test_rccl_single_rank_comm_and_device_store():
     comm.broadcast([buf], [0])
     assert np.array_equal(buf.download(), a)
     assert np.array_equal(comm.allreduce_max([1.5, -2.0]), [1.5, -2.0])
+    # the exchange step's order: an export queued on the engine stream, then the broadcast behind an event
+    # recorded there (acmmp_comm_after), as pipeline.RcclExchange and bench.depth_exchange do
+    ds = small_dataset(48, 24, 2)
+    with capi.Context(0) as ctx:
+        p = types.default_params(num_images=2, depth_min=float(ds.cameras[0]["depth_min"]) * 0.6,
+                                 depth_max=float(ds.cameras[0]["depth_max"]) * 1.2)
+        ctx.set_params(p)
+        ctx.upload_views([ds.images[0], ds.images[1]], np.array([ds.cameras[0], ds.cameras[1]]))
+        ctx.run_patchmatch(5)
+        planes, _ = ctx.download()
+        dbuf = capi.DeviceBuffer(0, planes.shape[:2])
+        ctx.export_depth(dbuf)
+        comm.after(ctx)
+        comm.broadcast([dbuf], [0])
+        assert_bitwise_equal(dbuf.download(), planes[..., 3], "exported depth after the broadcast")
+        dbuf.free()
     comm.close()
     buf.free()
 
