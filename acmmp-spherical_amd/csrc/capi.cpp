@@ -884,6 +884,13 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     // 6.7e-5, at 1280x640, R = 5 spanning 1.25x the angle, 8.5e-3).  patch_size 21 / increment 4 also
     // gives 6x6 samples but spans twice the angle: it projects every sample below 3200x1600.
     kp.interp = c->model == kSphere && nside == 6 && 1600LL * R <= 5LL * c->W && 800LL * R <= 5LL * c->H;
+    // ACMMP_INTERP=0 projects every sample in the fast mode too (the per-sample fast arithmetic the
+    // interpolation is gated against, tests/test_gpu_fastmath.py T2); read per run
+    if (const char* e = std::getenv("ACMMP_INTERP")) kp.interp = kp.interp && std::atoi(e) != 0;
+    // fast pinhole: each sample's source point from the per-view homogeneous affine form (ncc_chunk);
+    // ACMMP_PIN_HOMOG=0 projects it through depth and point per sample instead (A/B, tests)
+    kp.homog = 1;
+    if (const char* e = std::getenv("ACMMP_PIN_HOMOG")) kp.homog = std::atoi(e) != 0;
     kp.rows = std::min(c->H, 32 * (((c->H / 2) + 15) / 16));
     kp.row_lo = 0; kp.row_hi = kp.rows;
     kp.init_lo = 0; kp.init_hi = c->H;
@@ -918,20 +925,22 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     HIP_TRY(c, dreserve(c->d_spatial, c->spatial_cap, static_cast<size_t>(c->model == kSphere ? c->H : 1) * kp.S));
     HIP_TRY(c, launch_spatial_table(kp, c->d_spatial, c->stream));
     // half-sweep scratch slab: carve the pieces of engine.h's KParams out of one allocation
-    size_t off[13];
+    size_t off[16];
     {
         const size_t VP = static_cast<size_t>(kp.V) * Pc;
-        const size_t sizes[12] = {sizeof(float) * 8 * VP, sizeof(int) * 8 * Pc,
+        const size_t sizes[15] = {sizeof(float) * 8 * VP, sizeof(int) * 8 * Pc,
                                   sizeof(float4) * 5 * Pc, sizeof(float) * 5 * Pc, sizeof(float) * 5 * Pc,
                                   sizeof(PixState) * Pc, sizeof(float) * VP, sizeof(float) * VP,
-                                  sizeof(float) * 5 * VP, sizeof(uint32_t) * 5 * Pc, sizeof(unsigned),
-                                  sizeof(float4) * Pc};
+                                  sizeof(float) * 5 * VP, sizeof(uint32_t) * (5 * Pc + 256),
+                                  sizeof(unsigned) * (Pc / 51 + 2),
+                                  sizeof(float4) * Pc, sizeof(uint32_t) * kNbFixPerPixel * Pc, sizeof(unsigned),
+                                  sizeof(unsigned) * (Pc / 51 + 3)};
         off[0] = 0;
-        for (int k = 0; k < 12; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
+        for (int k = 0; k < 15; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
     }
-    if (c->scratch_bytes < off[12]) {
-        HIP_TRY(c, dalloc(c->d_scratch, off[12]));
-        c->scratch_bytes = off[12];
+    if (c->scratch_bytes < off[15]) {
+        HIP_TRY(c, dalloc(c->d_scratch, off[15]));
+        c->scratch_bytes = off[15];
     }
     kp.cams = c->d_cams;
     kp.tex16 = c->tex16;
@@ -961,6 +970,14 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.surv = reinterpret_cast<uint32_t*>(c->d_scratch + off[9]);
     kp.surv_count = reinterpret_cast<unsigned*>(c->d_scratch + off[10]);
     kp.psum = reinterpret_cast<float4*>(c->d_scratch + off[11]);
+    // queue of k_eval_nb's deferred interpolation fallbacks (pixel << 8 | hypothesis << 5 | view: colour
+    // grids below 2^24 pixels); a full queue sends the rest back to the inline fallback
+    const char* e_fix = std::getenv("ACMMP_NB_FIX");          // ACMMP_NB_FIX=0: inline fallbacks (A/B)
+    const bool fixq = Pc < (static_cast<size_t>(1) << 24) && !(e_fix && std::atoi(e_fix) == 0);
+    kp.nbfix = fixq ? reinterpret_cast<uint32_t*>(c->d_scratch + off[12]) : nullptr;
+    kp.nbfix_count = reinterpret_cast<unsigned*>(c->d_scratch + off[13]);
+    kp.surv_pre = reinterpret_cast<unsigned*>(c->d_scratch + off[14]);
+    kp.nbfix_cap = fixq ? static_cast<unsigned>(kNbFixPerPixel * Pc) : 0u;
     kp.ref_split = ref_split_point(kp.V, Pc);
     if (!c->d_work) HIP_TRY(c, dalloc(c->d_work, 256));
     kp.work = c->d_work;

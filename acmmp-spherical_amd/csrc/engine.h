@@ -26,6 +26,7 @@ namespace acmmp {
 constexpr int kPinhole = 0;
 constexpr int kSphere = 11;
 constexpr int kMaxViews = 32;       // cost_vector[32], uint32 view bitmask (ACMMP.cu:522,1153)
+constexpr int kNbFixPerPixel = 8;   // queue entries per colour-grid pixel for k_eval_nb's deferred fallbacks
 
 struct DevCam {
     // The fields the fast-math sample loop reads come first, contiguous and 16-byte aligned, so each
@@ -49,18 +50,18 @@ struct DevCam {
     float Hm1f;                     // H - 1 as float (SPHERE row clamp)
     int Wm1;                        // W - 1 (texel clamp)
     int pitch4;                     // bytes per padded row
+    float Hf;                       // H as float (pinhole in-image test)
+    int Hm1;                        // H - 1 (texel clamp)
     // the rest
     int model, W, H, img_pitch;     // img_pitch: floats per padded row (W + 2)
     float R[9];
     float t[3];
     float K[9];
     float inv_fx, inv_fy;           // 1/K[0], 1/K[4]  (pinhole world point)
-    float Hf;
     float C[3];                     // camera centre -(R^T t), computed like ACMMP.cu:592-594
     long long dep_off;              // float offset of the geom depth map (row-major)
     int dep_w, dep_h;
     int img_bytes;                  // bytes of the padded image (buffer descriptor range)
-    int Hm1;                        // H - 1 (texel clamp)
     const float* img_base;          // device address of padded texel (-1,-1) (buffer descriptor base)
 };
 
@@ -83,6 +84,7 @@ struct KParams {
     int W, H, Wh, N, V;             // ref size, colour row width ceil(W/2), images, source views
     int R, inc, nside, S;           // patch radius, radius_increment, offsets per axis, samples
     int interp;                     // fast SPHERE k_eval_nb interpolates sample coordinates
+    int homog;                      // fast pinhole staged chunks: homogeneous sample points
     int rows;                       // rows the reference's checkerboard grid covers
     // row ranges (full image by default; a row band in the split latency mode, acmmp_band_*):
     int row_lo, row_hi;             // colour-grid rows the half-sweep kernels update, within [0, rows)
@@ -132,9 +134,15 @@ struct KParams {
     // drops the ones whose partial aggregate already cannot beat cost_now, and queues the rest
     // (ci * 8 + candidate) for k_eval_ref_tail, which adds views [ref_split, V).  0 = no split.
     int ref_split;
-    uint32_t* surv;                 // [5 * Pc] queued candidates
-    unsigned* surv_count;           // queue length (zeroed before each k_eval_ref)
+    uint32_t* surv;                 // queued candidates: kRefSlots (255) slots per k_eval_ref block
+    unsigned* surv_count;           // [k_eval_ref blocks] slots used (zeroed before each k_eval_ref)
+    unsigned* surv_pre;             // [k_eval_ref blocks + 1] their exclusive prefix (k_tail_scan)
     float4* psum;                   // [Pc] (patch sum w, sum w r, sum w r^2, centre texel) for the tail
+    // k_eval_nb's deferred interpolation fallbacks (ncc_chunk, k_nb_fix): pixel << 8 | hypothesis << 5 |
+    // view; null = none (fallbacks inline)
+    uint32_t* nbfix;
+    unsigned* nbfix_count;
+    unsigned nbfix_cap;
 };
 
 // Per-half-sweep output buffers of the colour being updated.

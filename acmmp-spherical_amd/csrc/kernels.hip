@@ -493,6 +493,44 @@ __device__ __forceinline__ Tap fetch_tap(__amdgpu_buffer_rsrc_t rs, Cam& c, floa
     return t;
 }
 
+// Pinhole: ix = cvt_flr_i32(x), iy = cvt_flr_i32(y) of the sample; the sample is in the source image
+// (ProjectonCamera's caller, ACMMP.cu:470-473: !(x < 0 || x >= W || y < 0 || y >= H)) exactly when both are
+// in [0, W-1] / [0, H-1] as unsigned compares -- the same verdict for every float, NaN included (the float
+// compares pass a NaN coordinate, and v_cvt_flr_i32_f32 maps NaN to 0) and +-inf / out-of-int-range values
+// (saturated).  Two compares against the integers the fetch needs anyway, instead of four float ones.
+template <typename Cam>
+__device__ __forceinline__ bool pin_in_image(Cam& c, int ix, int iy) {
+    return (static_cast<unsigned>(ix) <= static_cast<unsigned>(c.Wm1)) &
+           (static_cast<unsigned>(iy) <= static_cast<unsigned>(c.Hm1));
+}
+
+// The pinhole footprint at (ix, iy) = floor(x, y) without fetch_tap's clamps: an in-image sample's
+// footprint is inside the padded image, and an out-of-image one is never accumulated (its weight and
+// texel are selected to zero), so its offset may be anything -- the buffer descriptor's range check
+// returns 0 for an offset past the image, and one inside it reads some texel that is discarded.  The
+// row +1 of the padding goes into the scalar offsets.  Same addresses and weights as fetch_tap for
+// every in-image sample.
+template <int TEX>
+__device__ __forceinline__ Tap fetch_tap_pin_p(__amdgpu_buffer_rsrc_t rs, int pitch4, float x, float y, int ix, int iy) {
+    Tap t;
+    const unsigned off = mad_u24(static_cast<unsigned>(iy), pitch4, (static_cast<unsigned>(ix) << 2) + 4u);
+    if (TEX == 1) {
+        t.a = __builtin_amdgcn_fractf(x);           // = x - floor(x) for x >= 0 (fetch_tap's note)
+        t.b = __builtin_amdgcn_fractf(y);
+        t.pw = __builtin_amdgcn_raw_buffer_load_b64(rs, off, pitch4, 0);
+        return t;
+    }
+    t.a = x - floorf(x);
+    t.b = y - floorf(y);
+    t.top = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, pitch4, 0));
+    t.bot = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 2 * pitch4, 0));
+    return t;
+}
+template <int TEX, typename Cam>
+__device__ __forceinline__ Tap fetch_tap_pin(__amdgpu_buffer_rsrc_t rs, Cam& c, float x, float y, int ix, int iy) {
+    return fetch_tap_pin_p<TEX>(rs, c.pitch4, x, y, ix, iy);
+}
+
 // fmaf(a, d, (float)lo(v)) in one v_fma_mix_f32
 __device__ __forceinline__ float f16_fma_lo(float a, float d, unsigned v) {
     float r;
@@ -600,9 +638,41 @@ __device__ __forceinline__ float ncc_cost(float sbw, f32x2 srrr, f32x2 ssrs, flo
     return out;
 }
 
+// One SPHERE view's (sum w s, sum w r s) and sum w s s with every one of the 36 samples projected in the
+// fast arithmetic, in patch order (ACMMP.cu:456-498): the interpolated loop's fallback, inline in
+// ncc_chunk or deferred to k_nb_fix.  sample(s, rw, r): sample s's (ray, w) and reference texel, from the
+// staged patch or recomputed -- the same values either way, so the same bits.
+template <int TEX, typename Cam, typename SampleF>
+__device__ __forceinline__ void sphere_view_sums(Cam& c, float4 ph, __amdgpu_buffer_rsrc_t rs, SampleF&& sample,
+                                                 f32x2& ssrs, float& sss) {
+    ssrs = splat2(0.f);
+    sss = 0.f;
+#pragma nounroll
+    for (int s = 0; s < 36; ++s) {
+        float4 rw;
+        float r;
+        sample(s, rw, r);
+        const float dep = depth_from_plane_fast(ph, rw);
+        float x, y;
+        project_fast<kSphere>(c, cam_point_fast<kSphere>(c, 0, 0, dep, rw), x, y);
+        x = fmaf(-floorf(x * c.invW), c.Wf, x);
+        y = __builtin_amdgcn_fmed3f(y, 0.0f, c.Hm1f);
+        const Tap t = fetch_tap<TEX, true>(rs, c, x, y);
+        const float w = rw.w;
+        const f32x2 wwr = (f32x2){w, w * r};
+        const float sp = lerp_tap<TEX>(t);
+        ssrs = pk_fma(wwr, splat2(sp), ssrs);
+        const float ws = w * sp;
+        sss = fmaf(ws, sp, sss);
+    }
+}
+
+// fixkey: k_eval_nb's (pixel << 8 | hypothesis << 5) for deferring interpolation fallbacks to k_nb_fix;
+// ~0u: none (every other caller, the fallback runs inline)
 template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM = 0, bool FULL = false>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
-                                          const int (&vlist)[VB], int nv_rt, float (&cost)[VB]) {
+                                          const int (&vlist)[VB], int nv_rt, float (&cost)[VB],
+                                          uint32_t fixkey = ~0u) {
     // FULL: every view of the chunk present (compile-time); otherwise a wave-uniform count, kept in an
     // SGPR so the per-view guards are scalar branches (without it they were lane masks round-tripped
     // through a VGPR: two VALU per view-sample)
@@ -679,14 +749,22 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     constexpr int G = PIPE ? VB : 1;
     // accumulate view v's sample (ACMMP.cu:488-498): texel tap T of a sample with weight W_,
     // (w, w r) = WWR_ and reference texel R_
+// Pinhole: a sample outside the source image (ok false) adds nothing (ACMMP.cu:470-473); instead of a
+// branch per view-sample its weight and texel are selected to zero -- fma(0, 0, s) and s + 0 return s
+// for the non-negative sums, so the same bits as skipping it
 #define ACMMP_ACCUMULATE_T(v, T, W_, WWR_, R_, OK_)                          \
     do {                                                             \
         const float sp = lerp_tap<TEX>(T);                           \
-        if (MODEL == kSphere ? has(v) : (OK_)) {                     \
-            if (MODEL == kPinhole) {                                 \
-                sbw[v] += (W_);                                      \
-                srrr[v] = pk_fma(WWR_, splat2(R_), srrr[v]);         \
-            }                                                        \
+        if (MODEL == kPinhole) {                                     \
+            const bool ok_ = (OK_);                                  \
+            const f32x2 wwr_ = ok_ ? (WWR_) : splat2(0.f);           \
+            const float sp_ = ok_ ? sp : 0.f;                        \
+            sbw[v] += wwr_.x;                                        \
+            srrr[v] = pk_fma(wwr_, splat2(R_), srrr[v]);             \
+            ssrs[v] = pk_fma(wwr_, splat2(sp_), ssrs[v]);            \
+            const float ws = wwr_.x * sp_;                           \
+            sss[v] = fmaf(ws, sp_, sss[v]);                          \
+        } else if (has(v)) {                                         \
             ssrs[v] = pk_fma(WWR_, splat2(sp), ssrs[v]);             \
             const float ws = (W_) * sp;                              \
             sss[v] = fmaf(ws, sp, sss[v]);                           \
@@ -713,6 +791,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             constexpr float kL4[4] = {0.06666667f, -0.6666667f, 1.3333334f, 0.26666667f};
             constexpr int kNode[4] = {0, 2, 3, 5};
             constexpr float kSpreadMax = 64.0f;     // source pixels spanned by the corner nodes (see below)
+            uint32_t rough = 0u;                        // views whose nodes spread too far (below)
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
                 if (!has(v)) continue;
@@ -722,20 +801,22 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 float x00 = 0.f;                            // the first node's x (set below)
                 // one patch column's six samples from its four row nodes (x, y): the bilinear tap and the
                 // sums of ACMMP.cu:488-498
-                auto column = [&](int ci, const float (&nx)[4], const float (&ny)[4]) {
+                // (x, y) of a sample as one packed pair: the interpolation's x and y share their Lagrange
+                // weights, so each term is one v_pk_fma_f32 (the same fma order per coordinate as the
+                // scalar chains, so the same bits)
+                auto column = [&](int ci, const f32x2 (&nd)[4]) {
                     asm volatile("" ::: "memory");
 #pragma unroll
                     for (int cj = 0; cj < 6; ++cj) {
-                        float x, y;
+                        f32x2 xy;
                         if (cj == 0 || cj == 2 || cj == 3 || cj == 5) {
-                            const int b = cj == 0 ? 0 : (cj == 2 ? 1 : (cj == 3 ? 2 : 3));
-                            x = nx[b];
-                            y = ny[b];
+                            xy = nd[cj == 0 ? 0 : (cj == 2 ? 1 : (cj == 3 ? 2 : 3))];
                         } else {
                             const float* L = cj == 1 ? kL1 : kL4;
-                            x = fmaf(L[3], nx[3], fmaf(L[2], nx[2], fmaf(L[1], nx[1], L[0] * nx[0])));
-                            y = fmaf(L[3], ny[3], fmaf(L[2], ny[2], fmaf(L[1], ny[1], L[0] * ny[0])));
+                            xy = pk_fma(splat2(L[3]), nd[3], pk_fma(splat2(L[2]), nd[2],
+                                        pk_fma(splat2(L[1]), nd[1], splat2(L[0]) * nd[0])));
                         }
+                        float x = xy.x, y = xy.y;
                         const float4 q = pt.rw[(ci * 6 + cj) * pt.stride];
                         const float w = q.z, r = q.w;
                         x += x00;
@@ -756,7 +837,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 // instead of 4, profiles/r03_interp_form_ab.txt) -- with x as offsets from the first node,
                 // unwrapped across the seam: small numbers, so the interpolation's rounding stays far below
                 // the positions' own
-                float nx[4][4], ny[4][4];
+                f32x2 nd[4][4];                             // (x - x00 unwrapped, y) per node
 #pragma unroll
                 for (int a = 0; a < 4; ++a) {
 #pragma unroll
@@ -768,12 +849,12 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         project_fast<MODEL>(c, make_float3(rw.x * dep, rw.y * dep, rw.z * dep), x, y);
                         if (a == 0 && b == 0) {
                             x00 = x;
-                            nx[a][b] = 0.0f;
+                            nd[a][b].x = 0.0f;
                         } else {
                             const float dx = x - x00;
-                            nx[a][b] = fmaf(-rintf(dx * c.invW), c.Wf, dx);
+                            nd[a][b].x = fmaf(-rintf(dx * c.invW), c.Wf, dx);
                         }
-                        ny[a][b] = y;
+                        nd[a][b].y = y;
                     }
                 }
                 // The interpolation holds where the source mapping is smooth over the patch.  Where the four
@@ -784,58 +865,158 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 // bit).  float64 study (tests/np_interp.py, tests/test_interp_design.py): with the test, the
                 // interpolated NCC stays within 4e-5 of the projected one on every query tried from 1600x800
                 // up, pole-adjacent and random planes included; without it the tail reached 0.6.
-                const float sx_ = fmaxf(fmaxf(nx[0][3], nx[3][0]), fmaxf(nx[3][3], 0.0f)) -
-                                  fminf(fminf(nx[0][3], nx[3][0]), fminf(nx[3][3], 0.0f));
-                const float sy_ = fmaxf(fmaxf(ny[0][0], ny[0][3]), fmaxf(ny[3][0], ny[3][3])) -
-                                  fminf(fminf(ny[0][0], ny[0][3]), fminf(ny[3][0], ny[3][3]));
+                const float sx_ = fmaxf(fmaxf(nd[0][3].x, nd[3][0].x), fmaxf(nd[3][3].x, 0.0f)) -
+                                  fminf(fminf(nd[0][3].x, nd[3][0].x), fminf(nd[3][3].x, 0.0f));
+                const float sy_ = fmaxf(fmaxf(nd[0][0].y, nd[0][3].y), fmaxf(nd[3][0].y, nd[3][3].y)) -
+                                  fminf(fminf(nd[0][0].y, nd[0][3].y), fminf(nd[3][0].y, nd[3][3].y));
                 const bool smooth = fmaxf(sx_, sy_) <= kSpreadMax;
+                rough |= smooth ? 0u : (1u << v);
                 // the samples re-read (w, r) from LDS rather than keep the nodes' reads live across the
                 // projections (merged, they spilled 210 VGPRs)
                 asm volatile("" ::: "memory");
 #pragma unroll
-                for (int a = 0; a < 4; ++a) column(kNode[a], nx[a], ny[a]);
+                for (int a = 0; a < 4; ++a) column(kNode[a], nd[a]);
                 // the interpolated columns 1 and 4 at the node rows, formed after the node columns (fewer
                 // values live across them)
-                float c1x[4], c1y[4], c4x[4], c4y[4];
+                f32x2 c1[4], c4[4];
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
-                    c1x[b] = c1y[b] = c4x[b] = c4y[b] = 0.f;
+                    c1[b] = c4[b] = splat2(0.f);
 #pragma unroll
                     for (int a = 0; a < 4; ++a) {
-                        c1x[b] = fmaf(kL1[a], nx[a][b], c1x[b]);
-                        c1y[b] = fmaf(kL1[a], ny[a][b], c1y[b]);
-                        c4x[b] = fmaf(kL4[a], nx[a][b], c4x[b]);
-                        c4y[b] = fmaf(kL4[a], ny[a][b], c4y[b]);
+                        c1[b] = pk_fma(splat2(kL1[a]), nd[a][b], c1[b]);
+                        c4[b] = pk_fma(splat2(kL4[a]), nd[a][b], c4[b]);
                     }
                 }
-                column(1, c1x, c1y);
-                column(4, c4x, c4y);
-                // lanes whose corners spread too far redo the view with every sample projected (the
-                // !interp_done loop's arithmetic and order), after the interpolated pass so that no node
-                // stays live across the branch (as an if / else around the columns: 259 VGPRs spilled)
-                if (!smooth) {
-                    ssrs[v] = splat2(0.f);
-                    sss[v] = 0.f;
-#pragma nounroll
-                    for (int s = 0; s < 36; ++s) {
+                column(1, c1);
+                column(4, c4);
+                __builtin_amdgcn_sched_barrier(0);           // one view's nodes live at a time
+            }
+            // Lanes whose corners spread too far take the view with every sample projected (the
+            // !interp_done loop's arithmetic and order).  In k_eval_nb (fixkey set) they are queued for
+            // k_nb_fix instead, which recomputes those (pixel, hypothesis, view) costs the same way after
+            // the launch: done here, one such lane made its whole wave run the 36 projections (3-6% of
+            // lanes, so most waves: k_eval_nb +28%).  The inline form stays for the test hook and a full
+            // queue.  After the view loop, with no node live (inside it the queue's code spilled).
+#pragma unroll
+            for (int v = 0; v < VB; ++v) {
+                if (!has(v)) continue;
+                bool redo = (rough >> v) & 1u;
+                if (fixkey != ~0u) {
+                    const unsigned long long b = __ballot(redo);
+                    if (b) {
+                        const int lane = __lane_id();
+                        const int leader = __ffsll(static_cast<long long>(b)) - 1;
+                        unsigned base = 0u;
+                        if (lane == leader) base = atomicAdd(kp.nbfix_count, static_cast<unsigned>(__popcll(b)));
+                        base = __shfl(base, leader);
+                        const unsigned slot = base + static_cast<unsigned>(__popcll(b & ((1ull << lane) - 1ull)));
+                        if (redo && slot < kp.nbfix_cap) {
+                            kp.nbfix[slot] = fixkey | static_cast<uint32_t>(cv[v] - 1);
+                            redo = false;
+                        }
+                    }
+                }
+                if (redo) {
+                    ConstCam& c = PCV(v);
+                    const __amdgpu_buffer_rsrc_t rs =
+                        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000);
+                    sphere_view_sums<TEX>(c, ph, rs, [&](int s, float4& rw, float& r) {
                         const int jj = s - (s / 6) * 6;
                         const float4 q = pt.rw[s * pt.stride];
-                        const float4 rw = make_float4(q.x, pt.rr[jj * pt.stride], q.y, q.z);
-                        const float dep = depth_from_plane_fast(ph, rw);
-                        float x, y;
-                        project_fast<MODEL>(c, cam_point_fast<MODEL>(c, 0, 0, dep, rw), x, y);
-                        x = fmaf(-floorf(x * c.invW), c.Wf, x);
-                        y = __builtin_amdgcn_fmed3f(y, 0.0f, c.Hm1f);
-                        const Tap t = fetch_tap<TEX, true>(rs, c, x, y);
-                        const float w = rw.w, r = q.w;
-                        const f32x2 wwr = (f32x2){w, w * r};
-                        const float sp = lerp_tap<TEX>(t);
-                        ssrs[v] = pk_fma(wwr, splat2(sp), ssrs[v]);
-                        const float ws = w * sp;
-                        sss[v] = fmaf(ws, sp, sss[v]);
+                        rw = make_float4(q.x, pt.rr[jj * pt.stride], q.y, q.z);
+                        r = q.w;
+                    }, ssrs[v], sss[v]);
+                }
+            }
+        }
+    }
+    // Fast pinhole chunks of the staged layouts: the source point of sample (i, j) as one homogeneous
+    // vector per view.  The reference's point is depth_s * v_s with v_s = ((x+i - cx) / fx, (y+j - cy) / fy, 1)
+    // (Get3DPointonWorld_cu's pinhole branch, ACMMP.cu:579-581) and depth_s = -w / D_s, D_s = n . r_s for the
+    // normalised table ray r_s (ACMMP.cu:187-193); its source image point FR (depth_s v_s) + Ft, scaled by
+    // w / depth_s (a projective scale: the same x / z and y / z), is
+    //     w FR v_s - D_s Ft,     FR v_s = FR v_0 + i FR e_x / fx + j FR e_y / fy,
+    // affine in (i, j).  So per view the lane forms h0 = w FR v_0 and the steps hi = w FR e_x / fx,
+    // hj = w FR e_y / fy once per chunk, and per sample fma(j, hj, fma(i, hi, h0)) - D_s Ft: 4 VALU per
+    // view-sample for the point (project_fast: 6 plus 2 moves of Ft, plus the depth division and the point
+    // per sample), and no FR in scalar registers across the loop (at 4 views they spilled).  The
+    // reference's depth clamp (|D_s| < 1e-6: depth 1e6) is the scale w * 1e-6 in place of -D_s.
+    constexpr bool kHomog = FM && MODEL == kPinhole && STAGED == 3;
+    if constexpr (kHomog) if (kp.homog) {
+        interp_done = true;
+        ConstCam& c0 = ccams[0];
+        const float v0x = (static_cast<float>(px) - c0.K[2]) * c0.inv_fx;
+        const float v0y = (static_cast<float>(py) - c0.K[5]) * c0.inv_fy;
+        float h0[VB][3], hi[VB][3], hj[VB][3];
+#pragma unroll
+        for (int v = 0; v < VB; ++v) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                h0[v][r] = hi[v][r] = hj[v][r] = 0.f;
+                if (has(v)) {
+                    ConstCam& c = PCV(v);
+                    const float f0 = r < 2 ? c.FRxy[r] : c.FRz[0];        // FR[r][0]
+                    const float f1 = r < 2 ? c.FRxy[2 + r] : c.FRz[1];    // FR[r][1]
+                    const float f2 = r < 2 ? c.FRxy[4 + r] : c.FRz[2];    // FR[r][2]
+                    h0[v][r] = ph.w * fmaf(f1, v0y, fmaf(f0, v0x, f2));
+                    hi[v][r] = ph.w * (f0 * c0.inv_fx);
+                    hj[v][r] = ph.w * (f1 * c0.inv_fy);
+                }
+            }
+        }
+        // each view's image descriptor and bounds formed once, before the loop (built at their use, the
+        // compiler re-read their fields through scalar loads per sample)
+        __amdgpu_buffer_rsrc_t rsv[VB];
+        int wm1[VB], hm1[VB], p4[VB];
+#pragma unroll
+        for (int v = 0; v < VB; ++v) {
+            ConstCam& c = PCV(v);
+            rsv[v] = TEX == 1
+                ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000)
+                : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(c.img_base), 0, c.img_bytes, 0x00020000);
+            wm1[v] = uniform_int(c.Wm1);
+            hm1[v] = uniform_int(c.Hm1);
+            p4[v] = uniform_int(c.pitch4);
+        }
+        const float w_clamp = ph.w * 1e-6f;
+        int s = 0;
+        for (int i = -R; i <= R; i += inc) {
+            const float fi = static_cast<float>(i);
+            float hr[VB][3];
+#pragma unroll
+            for (int v = 0; v < VB; ++v)
+#pragma unroll
+                for (int r = 0; r < 3; ++r) hr[v][r] = fmaf(fi, hi[v][r], h0[v][r]);
+            for (int j = -R; j <= R; j += inc, ++s) {
+                const float fj = static_cast<float>(j);
+                const float4 q = pt.rw[s * pt.stride];      // (r_s, w_s)
+                const float r = pt.rr[s * pt.stride];
+                const float D = dot3(ph.x, ph.y, ph.z, q.x, q.y, q.z);
+                const float sc = fabsf(D) < 1e-6f ? w_clamp : -D;
+                const float w = q.w;
+                const f32x2 wwr = (f32x2){w, w * r};
+                Tap tap[VB];
+                bool ok[VB];
+#pragma unroll
+                for (int v = 0; v < VB; ++v) {
+                    ok[v] = false;
+                    if (has(v)) {
+                        ConstCam& c = PCV(v);
+                        f32x2 t = pk_fma(splat2(fj), (f32x2){hj[v][0], hj[v][1]}, (f32x2){hr[v][0], hr[v][1]});
+                        float tz = fmaf(fj, hj[v][2], hr[v][2]);
+                        t = pk_fma(splat2(sc), (f32x2){c.Ft[0], c.Ft[1]}, t);
+                        tz = fmaf(sc, c.Ft[2], tz);
+                        const f32x2 o = t * splat2(__builtin_amdgcn_rcpf(tz));
+                        const int ix = cvt_flr_i32(o.x), iy = cvt_flr_i32(o.y);
+                        ok[v] = (static_cast<unsigned>(ix) <= static_cast<unsigned>(wm1[v])) &
+                                (static_cast<unsigned>(iy) <= static_cast<unsigned>(hm1[v]));   // pin_in_image
+                        tap[v] = fetch_tap_pin_p<TEX>(rsv[v], p4[v], o.x, o.y, ix, iy);
                     }
                 }
-                __builtin_amdgcn_sched_barrier(0);           // one view's nodes live at a time
+#pragma unroll
+                for (int v = 0; v < VB; ++v)
+                    if (has(v)) ACMMP_ACCUMULATE(v);
             }
         }
     }
@@ -888,16 +1069,18 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         if (FM) project_fast<MODEL>(c, P, sx, sy, kFtV ? ftv[v] : nullptr);
                         else project<MODEL>(c, P, sx, sy, sd);
                         ok[v] = true;
-                        if (MODEL == kSphere) {
-                            sx = fmaf(-floorf(sx * c.invW), c.Wf, sx);
-                            sy = FM ? __builtin_amdgcn_fmed3f(sy, 0.0f, c.Hm1f) : clamp0(sy, c.Hm1f);
-                        } else {
-                            ok[v] = !(sx < 0.0f || sx >= c.Wf || sy < 0.0f || sy >= c.Hf);
-                        }
                         const __amdgpu_buffer_rsrc_t rs = TEX == 1
                             ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000)
                             : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(c.img_base), 0, c.img_bytes, 0x00020000);
-                        tap[v] = fetch_tap<TEX, MODEL == kSphere>(rs, c, sx, sy);
+                        if (MODEL == kSphere) {
+                            sx = fmaf(-floorf(sx * c.invW), c.Wf, sx);
+                            sy = FM ? __builtin_amdgcn_fmed3f(sy, 0.0f, c.Hm1f) : clamp0(sy, c.Hm1f);
+                            tap[v] = fetch_tap<TEX, true>(rs, c, sx, sy);
+                        } else {
+                            const int ix = cvt_flr_i32(sx), iy = cvt_flr_i32(sy);
+                            ok[v] = pin_in_image(c, ix, iy);
+                            tap[v] = fetch_tap_pin<TEX>(rs, c, sx, sy, ix, iy);
+                        }
                         if (G == 1) ACMMP_ACCUMULATE(v);
                     }
                     // a full SPHERE chunk has no per-view branches; keep its views' code in view order
@@ -1007,7 +1190,7 @@ __device__ __forceinline__ float4 perturbed_normal(float4 v, float4 n, Rng& rs, 
 // Evaluate all source views of plane `ph` and hand each cost to f(view0, cost) in view order.
 template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM, typename F>
 __device__ __forceinline__ void for_all_views_t(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
-                                                uint32_t wave_mask, F&& f) {
+                                                uint32_t wave_mask, F&& f, uint32_t fixkey = ~0u) {
     int v = 0;
     const int V = kp.V;
     while (true) {
@@ -1028,9 +1211,9 @@ __device__ __forceinline__ void for_all_views_t(const KParams& kp, int px, int p
         if (nv == 0) break;
         float cost[VB];
         if ((MODEL == kSphere ? VB <= 2 : true) && VB > 1 && nv == VB)
-            ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM, true>(kp, px, py, pt, ph, vlist, nv, cost);
+            ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM, true>(kp, px, py, pt, ph, vlist, nv, cost, fixkey);
         else
-            ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM>(kp, px, py, pt, ph, vlist, nv, cost);
+            ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM>(kp, px, py, pt, ph, vlist, nv, cost, fixkey);
 #pragma unroll
         for (int k = 0; k < VB; ++k)
             if (k < nv) f(vlist[k] - 1, cost[k]);
@@ -1473,6 +1656,16 @@ constexpr int kEvalVB = 4;
 // k_eval_nb keeps every view's texels of a sample in flight (PIPE) in fast-math mode only, whose shorter
 // projection leaves the registers for it (r02 A/B: k_eval_nb 2.19 -> 2.06 ms; the exact mode -4%)
 constexpr bool kNbPipeExact = false, kNbPipeFast = true;
+// fast pinhole chunks (the homogeneous sample points of ncc_chunk): views per chunk (ACMMP_NB_PIN_VB
+// overrides at build time for A/B builds)
+#ifndef ACMMP_NB_PIN_VB
+#define ACMMP_NB_PIN_VB 4
+#endif
+template <int MODEL, int VB, int FM>
+constexpr int nb_vb() {
+    constexpr int cap = (MODEL == kPinhole && FM) ? ACMMP_NB_PIN_VB : kEvalVB;
+    return VB > cap ? cap : VB;
+}
 constexpr int kNbLanes = 8;                 // the 8 neighbour directions (the current plane's costs are cached)
 constexpr int kNbPix = 32;                  // pixels per 256-lane block
 
@@ -1575,6 +1768,7 @@ template <int MODEL, int VB>
 constexpr int ref_vb() { return (VB == 4 || (VB > 4 && MODEL == kSphere)) ? 2 : (VB > kEvalVB ? kEvalVB : VB); }
 constexpr int kRefLanes = 5;                // refinement candidates (ACMMP.cu:870)
 constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 lanes used)
+constexpr int kRefSlots = kRefPix * kRefLanes;  // survivor slots per k_eval_ref block
 
 // Adaptive checkerboard sampling of every pixel of the colour, one direction per grid row: the
 // direction is wave-uniform here, where inside k_eval_nb (lane = direction) a wave walks all eight
@@ -1620,8 +1814,41 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? 7 : 8) : 1) void k_ev
     const float4 ph = plane_at(kp, pos);
     const uint32_t all = kp.nb_views;
     float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
-    for_all_views_t<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
-        kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; });
+    const uint32_t fixkey = kp.nbfix ? (static_cast<uint32_t>(ci) << 8) | (static_cast<uint32_t>(h) << 5) : ~0u;
+    for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
+        kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; }, fixkey);
+}
+
+// The interpolation fallbacks k_eval_nb queued (ncc_chunk): each (pixel, hypothesis, view) cost with every
+// sample projected, the patch recomputed (make_patch: the staged values and sums, the same bits), over
+// the same hyp_cost entry k_eval_nb wrote.  One lane per entry, after every k_eval_nb launch of the
+// half-sweep and before k_select.
+template <int TEX>
+__global__ __launch_bounds__(256) void k_nb_fix(const KParams kp, const int colour) {
+    const unsigned n = min(*kp.nbfix_count, kp.nbfix_cap);
+    const long long Pc = kp.Pc;
+    typedef const __attribute__((address_space(4))) DevCam ConstCam;
+    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint32_t key = kp.nbfix[i];
+        const long long ci = key >> 8;
+        const int h = static_cast<int>((key >> 5) & 7u), v = static_cast<int>(key & 31u);
+        const int py = static_cast<int>(ci / kp.Wh);
+        const int px = 2 * static_cast<int>(ci - static_cast<long long>(py) * kp.Wh) + ((py + colour) & 1);
+        const float4 ph = plane_at(kp, kp.nbpos[h * Pc + ci]);
+        const Patch pt = make_patch<kSphere>(kp, px, py);
+        ConstCam& c = ((ConstCam*)(kp.cams))[v + 1];
+        const __amdgpu_buffer_rsrc_t rs = TEX == 1
+            ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000)
+            : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(c.img_base), 0, c.img_bytes, 0x00020000);
+        f32x2 ssrs;
+        float sss;
+        sphere_view_sums<TEX>(c, ph, rs, [&](int s, float4& rw, float& r) {
+            const int ii = s / kp.nside, jj = s - ii * kp.nside;
+            rw = patch_sample<kSphere>(kp, px, py, s, -kp.R + ii * kp.inc, -kp.R + jj * kp.inc, pt.center, r);
+        }, ssrs, sss);
+        kp.hyp_cost[(static_cast<long long>(h) * kp.V + v) * Pc + ci] =
+            ncc_cost(pt.sbw, (f32x2){pt.sref, pt.srr}, ssrs, sss);
+    }
 }
 
 // Joint view selection, aggregation, acceptance and refinement candidates (ACMMP.cu:1146-1311,
@@ -2026,25 +2253,77 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
     const bool done = !(st.flags & 1u) && !(partial < st.cost_now);
     kp.cand_cost[h * Pc + ci] = done ? partial : temp_cost;
     const unsigned long long b = __ballot(!done);
-    if (b) {                                                 // queue the wave's survivors
+    if (b) {                                                 // queue the wave's survivors in the block's slots
         const int lane = __lane_id();
         const int leader = __ffsll(static_cast<long long>(b)) - 1;
         unsigned base = 0u;
-        if (lane == leader) base = atomicAdd(kp.surv_count, static_cast<unsigned>(__popcll(b)));
+        if (lane == leader) base = atomicAdd(kp.surv_count + blockIdx.x, static_cast<unsigned>(__popcll(b)));
         base = __shfl(base, leader);
-        if (!done) kp.surv[base + __popcll(b & ((1ull << lane) - 1ull))] = static_cast<uint32_t>(ci * 8 + h);
+        if (!done)
+            kp.surv[static_cast<long long>(blockIdx.x) * kRefSlots + base + __popcll(b & ((1ull << lane) - 1ull))] =
+                static_cast<uint32_t>(ci * 8 + h);
     }
 }
 
+#if ACMMP_IN_TU(4)
+// k_eval_ref's per-block survivor counts -> their exclusive prefix surv_pre[0 .. nref] (surv_pre[nref] =
+// all survivors): one block, each thread a contiguous run of k_eval_ref blocks.
+__global__ __launch_bounds__(1024) void k_tail_scan(const KParams kp, const int nref) {
+    __shared__ unsigned part[1024];
+    const int t = threadIdx.x;
+    const int per = (nref + 1023) / 1024;
+    const int b0 = min(nref, t * per), b1 = min(nref, b0 + per);
+    unsigned sum = 0u;
+    for (int b = b0; b < b1; ++b) sum += kp.surv_count[b];
+    part[t] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {               // inclusive scan of the 1024 run sums
+        const unsigned add = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += add;
+        __syncthreads();
+    }
+    unsigned acc = part[t] - sum;
+    for (int b = b0; b < b1; ++b) {
+        kp.surv_pre[b] = acc;
+        acc += kp.surv_count[b];
+    }
+    if (t == 1023) kp.surv_pre[nref] = part[1023];
+}
+#endif  // ACMMP_IN_TU(4)
+
 // The queued candidates' views [ref_split, V) (one lane per candidate, patch samples recomputed),
 // continuing the aggregate's fma chain in view order from k_eval_ref's partial sum.
+// The survivors, in k_eval_ref block order (slots + surv_pre), are dealt to the XCDs as 8 contiguous
+// segments (blocks b and b + 8 share an XCD's L2): each XCD's resident blocks walk a window of a few
+// rows, so the source footprints its L2 holds are those rows' (a queue shared by all blocks, filled in
+// wave completion order, gave C3 a 58% L2 hit rate and 36 GB per launch), and every lane has a survivor
+// (per-k_eval_ref-block tail blocks left half their lanes idle).
 template <int MODEL, int VB, bool GEOM, int TF>
-__global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const int colour) {
-    const unsigned n = *kp.surv_count;
+__global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const int colour, const int nref) {
+    __shared__ int first_block;
+    const unsigned total = kp.surv_pre[nref];
+    const unsigned x = blockIdx.x & 7u, k = blockIdx.x >> 3, nk = gridDim.x >> 3;
+    const unsigned seg0 = static_cast<unsigned>(static_cast<unsigned long long>(total) * x / 8u);
+    const unsigned seg1 = static_cast<unsigned>(static_cast<unsigned long long>(total) * (x + 1u) / 8u);
     const long long Pc = kp.Pc;
     const int S = kp.ref_split;
-    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        const uint32_t rec = kp.surv[i];
+    for (unsigned c0 = seg0 + k * 256u; c0 < seg1; c0 += nk * 256u) {
+        if (threadIdx.x == 0) {                              // the k_eval_ref block holding survivor c0
+            int lo = 0, hi = nref - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (kp.surv_pre[mid] <= c0) lo = mid; else hi = mid - 1;
+            }
+            first_block = lo;
+        }
+        __syncthreads();
+        int b = first_block;
+        __syncthreads();
+        const unsigned i = c0 + threadIdx.x;
+        if (i >= seg1) continue;
+        while (kp.surv_pre[b + 1] <= i) ++b;
+        const uint32_t rec = kp.surv[static_cast<long long>(b) * kRefSlots + (i - kp.surv_pre[b])];
         const long long ci = rec >> 3;
         const int h = static_cast<int>(rec & 7u);
         const int py = static_cast<int>(ci / kp.Wh);
@@ -2414,6 +2693,11 @@ static int nb_view_chunk(const KParams& kp) {
 
 hipError_t launch_eval_nb(const KParams& kp0, int colour, hipStream_t s) {
     KParams kp = kp0;
+    // interpolation fallbacks deferred to k_nb_fix: fast SPHERE with interpolated coordinates only
+    const bool fix = kp.nbfix && kp.model == kSphere && kp.fast && kp.tex16 && kp.interp;
+    if (!fix) kp.nbfix = nullptr;
+    hipError_t e0 = hipSuccess;
+    if (fix && (e0 = hipMemsetAsync(kp.nbfix_count, 0, sizeof(unsigned), s)) != hipSuccess) return e0;
     const int chunk = nb_view_chunk(kp);
     for (int v0 = 0; v0 < kp.V; v0 += chunk) {
         const int v1 = std::min(kp.V, v0 + chunk);
@@ -2422,6 +2706,10 @@ hipError_t launch_eval_nb(const KParams& kp0, int colour, hipStream_t s) {
         kp.nb_count_work = v0 == 0;
         const hipError_t e = launch_eval_nb_views(kp, colour, s);
         if (e != hipSuccess) return e;
+    }
+    if (fix) {
+        k_nb_fix<1><<<1024, 256, 0, s>>>(kp, colour);
+        return hipGetLastError();
     }
     return hipSuccess;
 }
@@ -2447,7 +2735,7 @@ __global__ __launch_bounds__(256) void k_debug_nb(const KParams kp, int n, const
     const float4 ph = planes[k];
     float* o = out + k * kp.V;
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
-    for_all_views_t<MODEL, (VB > kEvalVB ? kEvalVB : VB), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
+    for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
         kp, px, py, pt, ph, all, [&](int v, float c) { o[v] = c; });
 }
 
@@ -2495,15 +2783,18 @@ hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s) {
     const size_t lds_ref = (kp.model == kSphere && pick_vb(kp.V) <= 4) ? sep_lds_bytes(kp.S, kp.nside, kRefPix)
                                                                        : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
     hipError_t e = hipSuccess;
-    if (kp.ref_split > 0 && (e = hipMemsetAsync(kp.surv_count, 0, sizeof(unsigned), s)) != hipSuccess) return e;
     const dim3 grd_ref = static_cast<unsigned>(cdiv(npix, kRefPix));
+    if (kp.ref_split > 0 && (e = hipMemsetAsync(kp.surv_count, 0, sizeof(unsigned) * grd_ref.x, s)) != hipSuccess) return e;
     if (kp.geom) ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, true, TF><<<grd_ref, 256, lds_ref, s>>>(kp, colour))));
     else ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, false, TF><<<grd_ref, 256, lds_ref, s>>>(kp, colour))));
     if (kp.ref_split > 0) {
-        // grid-stride over the queue (its length is known on the device only): at most 5 per pixel
-        const unsigned grd = static_cast<unsigned>(std::min<long long>(cdiv(5 * npix, 256), 8192));
-        if (kp.geom) ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, true, TF><<<grd, 256, 0, s>>>(kp, colour))));
-        else ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, false, TF><<<grd, 256, 0, s>>>(kp, colour))));
+        // the survivors' prefix over k_eval_ref blocks, then 8 x nk tail blocks (the queue's length is
+        // known on the device only: nk covers the largest possible queue, up to 256 blocks per XCD)
+        const int nref = static_cast<int>(grd_ref.x);
+        k_tail_scan<<<1, 1024, 0, s>>>(kp, nref);
+        const unsigned grd = 8u * static_cast<unsigned>(std::min<long long>(256, std::max<long long>(1, cdiv(static_cast<long long>(nref) * kRefSlots, 8 * 256))));
+        if (kp.geom) ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, true, TF><<<grd, 256, 0, s>>>(kp, colour, nref))));
+        else ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, false, TF><<<grd, 256, 0, s>>>(kp, colour, nref))));
     }
     return hipGetLastError();
 }

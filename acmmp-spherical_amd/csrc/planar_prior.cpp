@@ -74,22 +74,55 @@ public:
         t_.push_back({{n_real_, n_real_ + 1, n_real_ + 2}, {-1, -1, -1}, true});
     }
 
+    // Points go in along a Hilbert curve over the image: each insertion's walk and cavity stay local.
+    // (In the support points' own order -- 5-pixel column strips -- every point at the head of a strip
+    // re-triangulated the whole previous strip's hull fan: 36k points took 0.45 s, 112k 6 s.)  The
+    // Delaunay triangulation does not depend on the order except among co-circular points, whose
+    // diagonal any order may pick (cv::Subdiv2D's choice is not reproduced either).
     void run() {
-        for (int i = 0; i < n_real_; ++i) insert(i);
+        std::vector<std::pair<uint64_t, int>> key(n_real_);
+        long long ext = 1;
+        for (int i = 0; i < n_real_; ++i) ext = std::max(ext, std::max(p_[i].x, p_[i].y) + 1);
+        int bits = 1;
+        while ((1ll << bits) < ext) ++bits;
+        for (int i = 0; i < n_real_; ++i) key[i] = {hilbert(bits, p_[i].x, p_[i].y), i};
+        std::sort(key.begin(), key.end());
+        for (const auto& k : key) insert(k.second);
     }
 
-    // triangles without super vertices, in slot order
+    // triangles without super vertices, each rotated to start at its lowest point index (orientation
+    // kept) and listed in increasing (v0, v1, v2): an order that depends on the triangle set only
     std::vector<std::array<int, 3>> triangles() const {
         std::vector<std::array<int, 3>> out;
         for (const Tri& t : t_) {
             if (!t.alive) continue;
             if (t.v[0] >= n_real_ || t.v[1] >= n_real_ || t.v[2] >= n_real_) continue;
-            out.push_back({t.v[0], t.v[1], t.v[2]});
+            int r = 0;
+            if (t.v[1] < t.v[r]) r = 1;
+            if (t.v[2] < t.v[r]) r = 2;
+            out.push_back({t.v[r], t.v[(r + 1) % 3], t.v[(r + 2) % 3]});
         }
+        std::sort(out.begin(), out.end());
         return out;
     }
 
 private:
+    // distance of (x, y) along the Hilbert curve of a 2^bits x 2^bits grid (x, y >= 0)
+    static uint64_t hilbert(int bits, long long x, long long y) {
+        uint64_t d = 0;
+        for (long long s = 1ll << (bits - 1); s > 0; s >>= 1) {
+            const long long rx = (x & s) ? 1 : 0, ry = (y & s) ? 1 : 0;
+            d += static_cast<uint64_t>(s) * static_cast<uint64_t>(s) * static_cast<uint64_t>((3 * rx) ^ ry);
+            if (ry == 0) {                               // rotate the quadrant
+                if (rx == 1) { x = s - 1 - (x & (s - 1)); y = s - 1 - (y & (s - 1)); }
+                std::swap(x, y);
+            }
+            x &= s - 1;
+            y &= s - 1;
+        }
+        return d;
+    }
+
     int locate(const Pt& q) const {
         int t = last_;
         if (t < 0 || !t_[t].alive) {

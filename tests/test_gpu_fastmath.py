@@ -13,24 +13,33 @@ bit-identical, so it is held to the gates DESIGN.md §2.4 states, measured in pr
       can cross: 99.5% at the metric view), and for >= 99% of queries.
       (b) Pinhole: |fast - exact| <= 1e-4 for >= 99.5% of valid queries.  SPHERE: the
       binary32 noise floor of the reference's own arithmetic is far above 1e-4 -- the exact float32
-      path is within 1e-4 of float64 for only ~87% of valid queries at the metric view (few effective
-      samples under the sigma-in-radians weights, E[x^2] - E[x]^2 cancellation) -- so the gate is that
+      path is within 1e-4 of float64 for only ~91% of valid queries at the metric view (91.1% in
+      profiles/r03_fastmath_floor.json; few effective samples under the sigma-in-radians weights,
+      E[x^2] - E[x]^2 cancellation) -- so the gate is that
       fast departs from exact by > 1e-4 no more often than exact departs from float64, + 5 points.
       (c) No systematic accuracy loss: the fraction of queries where fast is farther from float64 than
       exact by > 1e-4 is at most the converse fraction + 3 points.
   T2  After RandomInitialization every plane is identical (same RNG draws) and costs agree within 1e-3
       for >= 99.5% (pinhole) / 99% (SPHERE) of pixels; after one black half-sweep >= 99.5% (pinhole) /
       98.5% (SPHERE) of pixels hold the same plane, and the flips are near ties: their median cost gap
-      is below 1e-4.
+      is below 1e-4.  Where the fast k_eval_nb interpolates SPHERE sample coordinates (>= 1600x800), the
+      98.5% holds for the per-sample fast arithmetic (ACMMP_INTERP=0) and the interpolated run may hold
+      at most 0.5 pt fewer same planes than it, with the same near-tie gate on its flips (the float64
+      study puts the interpolation's NCC effect below 1e-4, tests/test_interp_design.py; the flips it
+      adds are ties the binary32 noise already decides).
   T3  A full RunPatchMatch: >= 99% of finite depths within 1% of the exact mode's, ground-truth accuracy
       within +-0.5 points.  Geom, planar-prior and hierarchy passes from one shared state: T3, T2's init
       gates, and after one half-sweep >= 85% same plane (the hierarchy gate and the prior-restricted
       acceptance multiply near ties; a flip there selects by restricted cost or pre-cost, so its cost gap
       is not a tie measure and is not gated).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
+import np_interp as ni
 import np_reference as npr
 from acmmp import capi, scene, types
 
@@ -120,10 +129,12 @@ def check_t2(ctx, setup, seed, sphere, init=True, hs_min=None, gap_max=1e-4):
     ep, ec = run(ctx, "exact", seed, 1, False, setup)
     same = np.all(np.abs(fp - ep) <= 1e-4 * np.maximum(1.0, np.abs(ep)), axis=-1)
     floor = hs_min if hs_min is not None else (0.985 if sphere else 0.995)
-    assert same.mean() >= floor, same.mean()
+    assert same.mean() >= floor, (same.mean(), floor)
     fin = np.isfinite(fc) & np.isfinite(ec) & ~same
+    gap = float(np.median(np.abs(fc - ec)[fin])) if fin.sum() else 0.0
     if gap_max is not None and fin.sum() > 20:
-        assert np.median(np.abs(fc - ec)[fin]) < gap_max, np.median(np.abs(fc - ec)[fin])
+        assert gap < gap_max, gap
+    return float(same.mean()), gap
 
 
 def check_t3(ctx, setup, seed, gt):
@@ -174,8 +185,23 @@ def test_fast_mode_tolerance_at_baseline_configs(ctx, config, monkeypatch):
     p = params_for(sc)
     check_t1(ctx, sc, p, nq, seed=len(name), sphere=sphere)
     setup = plain_setup(sc, p)
-    check_t2(ctx, setup, 81, sphere)
+    H, W = sc.images[0].shape
+    report = {}
+    if sphere and ni.interp_enabled(W, H, p):
+        # T2 of the per-sample fast arithmetic against its floor, then the interpolated k_eval_nb against
+        # the per-sample one: its flips beyond those are near ties too (the median-gap gate), at most 0.5 pt
+        monkeypatch.setenv("ACMMP_INTERP", "0")
+        report["per_sample"] = check_t2(ctx, setup, 81, sphere)
+        monkeypatch.delenv("ACMMP_INTERP")
+        report["interpolated"] = check_t2(ctx, setup, 81, sphere, init=False, hs_min=report["per_sample"][0] - 0.005)
+    else:
+        report["per_sample"] = check_t2(ctx, setup, 81, sphere)
     check_t3(ctx, setup, 82, sc.gt_depth)
+    out_dir = os.environ.get("ACMMP_TEST_REPORT_DIR")
+    if out_dir:
+        os.makedirs(out_dir, exist_ok=True)
+        with open(os.path.join(out_dir, f"fastmath_t2_{name}.json"), "w") as fh:
+            json.dump({k: {"same_plane": v[0], "flip_median_cost_gap": v[1]} for k, v in report.items()}, fh, indent=1)
 
 
 PASS_RIGS = {"pinhole": lambda: scene.pinhole_scene(800, 600, n_src=10, seed=61, n_waves=24),

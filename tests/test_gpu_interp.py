@@ -131,3 +131,75 @@ def test_interpolated_k_eval_nb_per_query(ctx, name):
         os.makedirs(out_dir, exist_ok=True)
         with open(os.path.join(out_dir, f"interp_queries_{name}.json"), "w") as fh:
             json.dump(report, fh, indent=1)
+
+
+PIN_CONFIGS = {
+    "c2-pinhole-1600x1200-v10": lambda: scene.pinhole_scene(1600, 1200, n_src=10, seed=1234, n_waves=12),
+    "c5-pinhole-1920x1080-v20": lambda: scene.pinhole_scene(1920, 1080, n_src=20, seed=55, n_waves=12),
+}
+
+
+@pytest.mark.parametrize("name", list(PIN_CONFIGS))
+def test_pinhole_homogeneous_k_eval_nb_per_query(ctx, name, monkeypatch):
+    """The fast pinhole k_eval_nb forms each sample's source point as one homogeneous vector affine in the
+    patch offsets (ncc_chunk's kHomog loop) instead of depth -> point -> projection per sample: the same
+    point up to rounding.  Held per query against the same kernel with the per-sample projection
+    (ACMMP_PIN_HOMOG=0) and the exact mode: class agreement with exact; |fast - exact| <= 1e-4 as often as
+    the per-sample fast arithmetic's, within 0.5 pt (T1(b)'s pinhole 99.5% is the per-sample fast mode's
+    gate, test_gpu_fastmath.check_t1); and no systematic loss against the float64 per-sample restatement
+    (np_reference.bilateral_ncc, ACMMP.cu:405-516) beyond the exact mode's, + 3 pt (T1(c))."""
+    sc = PIN_CONFIGS[name]()
+    c0 = sc.cameras[0]
+    p = types.default_params(num_images=len(sc.images), depth_min=float(c0["depth_min"]) * 0.6,
+                             depth_max=float(c0["depth_max"]) * 1.2)
+    ctx.set_params(p)
+    ctx.upload_views(sc.images, sc.cameras)
+    H, W = sc.images[0].shape
+    rng = np.random.default_rng(91)
+    n = 96
+    px = rng.integers(6, W - 6, n).astype(np.int32)
+    py = rng.integers(6, H - 6, n).astype(np.int32)
+    planes = ni.near_surface_planes(sc, px, py, 8, seed=93)
+    ctx.set_math("fast")
+    f = ctx.debug_ncc_nb(px, py, planes)
+    monkeypatch.setenv("ACMMP_PIN_HOMOG", "0")
+    ps = ctx.debug_ncc_nb(px, py, planes)
+    monkeypatch.delenv("ACMMP_PIN_HOMOG")
+    ctx.set_math("exact")
+    e = ctx.debug_ncc_nb(px, py, planes)
+    assert np.any(f != ps)                                   # the homogeneous loop ran
+    agree_fe = float(np.mean((f >= 2.0) == (e >= 2.0)))
+    agree_pe = float(np.mean((ps >= 2.0) == (e >= 2.0)))
+    assert agree_fe >= min(agree_pe, 0.999) - 0.002, (agree_fe, agree_pe)
+    v = (f < 2.0) & (e < 2.0) & (ps < 2.0)
+    assert v.mean() > 0.3
+    dfe, dpe = np.abs(f - e)[v], np.abs(ps - e)[v]
+    frac_f, frac_p = float(np.mean(dfe <= 1e-4)), float(np.mean(dpe <= 1e-4))
+    assert frac_f >= frac_p - 0.005, (frac_f, frac_p)
+    # float64 on the first 2 planes of each pixel
+    V = len(sc.images) - 1
+    ref = np.full((n, 2, V), np.nan)
+    for q in range(n):
+        for h in range(2):
+            for k in range(1, V + 1):
+                ref[q, h, k - 1] = npr.bilateral_ncc(sc.images, sc.cameras, p, k, int(px[q]), int(py[q]),
+                                                     planes[q, h].astype(np.float64))
+    f2, p2, e2 = f[:, :2], ps[:, :2], e[:, :2]
+    valid = (f2 < 2.0) & (e2 < 2.0) & (p2 < 2.0) & (ref < 2.0)
+    df, dp, de = np.abs(f2 - ref)[valid], np.abs(p2 - ref)[valid], np.abs(e2 - ref)[valid]
+    fast_worse, exact_worse = float(np.mean(df > de + 1e-4)), float(np.mean(de > df + 1e-4))
+    assert fast_worse <= exact_worse + 0.03, (fast_worse, exact_worse)
+    d_fp = np.abs(f - ps)[v]
+    report = {"queries": int(f.size), "class_agree_homog_exact": agree_fe, "class_agree_per_sample_exact": agree_pe,
+              "frac_homog_within_1e-4_of_exact": frac_f, "frac_per_sample_within_1e-4_of_exact": frac_p,
+              "worst_homog_vs_exact": float(dfe.max()), "worst_per_sample_vs_exact": float(dpe.max()),
+              "worst_homog_vs_per_sample": float(d_fp.max()),
+              "frac_homog_within_1e-4_of_f64": float(np.mean(df <= 1e-4)),
+              "frac_per_sample_within_1e-4_of_f64": float(np.mean(dp <= 1e-4)),
+              "frac_exact_within_1e-4_of_f64": float(np.mean(de <= 1e-4)),
+              "homog_worse_than_exact_by_1e-4": fast_worse, "exact_worse_than_homog_by_1e-4": exact_worse}
+    out_dir = os.environ.get("ACMMP_TEST_REPORT_DIR")
+    if out_dir:
+        os.makedirs(out_dir, exist_ok=True)
+        with open(os.path.join(out_dir, f"pinhole_queries_{name}.json"), "w") as fh:
+            json.dump(report, fh, indent=1)
