@@ -29,7 +29,8 @@ EXPORTS = [
     "acmmp_last_kernel_timing", "acmmp_last_work", "acmmp_texel_bytes", "acmmp_set_math", "acmmp_get_math", "acmmp_jbu",
     "acmmp_debug_ncc", "acmmp_debug_geom", "acmmp_debug_ncc_nb",
     "acmmp_support_points", "acmmp_delaunay", "acmmp_prior_plane_params", "acmmp_depth_from_plane_param",
-    "acmmp_planar_prior_host", "acmmp_set_planar_prior_from_maps", "acmmp_download_planar_prior",
+    "acmmp_planar_prior_host", "acmmp_set_planar_prior_from_maps", "acmmp_set_planar_prior_from_state",
+    "acmmp_download_planar_prior",
     "acmmp_upload_depths_device", "acmmp_upload_views_device", "acmmp_export_depth", "acmmp_export_state", "acmmp_set_state_device", "acmmp_device_alloc", "acmmp_device_free", "acmmp_memcpy",
     "acmmp_comm_unique_id", "acmmp_comm_create", "acmmp_comm_destroy", "acmmp_comm_broadcast", "acmmp_comm_after",
     "acmmp_comm_allreduce_max", "acmmp_comm_band_exchange", "acmmp_run_patchmatch_band",
@@ -122,6 +123,7 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_fusion_destroy.argtypes = [vp]
     L.acmmp_planar_prior_host.argtypes = [vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]
     L.acmmp_set_planar_prior_from_maps.argtypes = [vp, vp, vp, C.c_float, C.c_float, vp]
+    L.acmmp_set_planar_prior_from_state.argtypes = [vp, C.c_float, C.c_float, vp]
     L.acmmp_download_planar_prior.argtypes = [vp, vp, vp]
     L.acmmp_image_cache_create.argtypes = [i32, C.c_size_t, C.POINTER(vp)]
     L.acmmp_image_cache_destroy.argtypes = [vp]
@@ -347,6 +349,16 @@ class Context:
         n = C.c_int(0)
         self._check(self.L.acmmp_set_planar_prior_from_maps(self.h, _p(d), _p(c), float(depth_min), float(depth_max),
                                                             C.byref(n)), "set_planar_prior_from_maps")
+        return n.value
+
+    def set_planar_prior_from_state(self, depth_min: float, depth_max: float) -> int:
+        """The planar block from this context's last RunPatchMatch output in HBM (support points on the
+        device, Delaunay and the planes on the host, raster + mask on the device): equal to
+        set_planar_prior_from_maps on the downloaded maps, without downloading them.  Returns the
+        triangle count."""
+        n = C.c_int(0)
+        self._check(self.L.acmmp_set_planar_prior_from_state(self.h, float(depth_min), float(depth_max), C.byref(n)),
+                    "set_planar_prior_from_state")
         return n.value
 
     def download_planar_prior(self):

@@ -599,7 +599,8 @@ class Pipeline:
         run_seed = self.seed + 7919 * self.pass_index + 31 * ref
         with self._timed("patchmatch"):
             e.run_patchmatch(run_seed)
-            planes, costs = e.download()
+            # a planar pass's first run feeds only the planar block, which a GPU context takes from HBM
+            planes, costs = (None, None) if (planar and self._state_planar(e)) else e.download()
         return dict(e=e, p=p, c0=c0, ref=ref, geom=geom, planar=planar, run_seed=run_seed, planes=planes, costs=costs)
 
     def _problem_tail(self, st):
@@ -608,7 +609,13 @@ class Pipeline:
         planes, costs = st["planes"], st["costs"]
         if planar:                                                   # main.cpp:113-187
             p["planar_prior"] = 1
-            if hasattr(e, "set_planar_prior_from_maps"):
+            if self._state_planar(e):
+                # support points on the device from the first run's maps in HBM, Delaunay + planes on the
+                # host, raster + mask on the device (== set_planar_prior_from_maps on the downloaded maps)
+                with self._timed("planar_prior"):
+                    e.set_params(p)
+                    e.set_planar_prior_from_state(float(p["depth_min"]), float(p["depth_max"]))
+            elif hasattr(e, "set_planar_prior_from_maps"):
                 # support points + Delaunay + planes on the host, raster + mask on the device
                 with self._timed("planar_prior"):
                     e.set_params(p)
@@ -643,6 +650,10 @@ class Pipeline:
                 io.write_dmb(os.path.join(d, "normals.dmb"), planes[..., :3])
                 io.write_dmb(os.path.join(d, "costs.dmb"), costs)
         return planes, costs
+
+    @staticmethod
+    def _state_planar(e):
+        return isinstance(e, capi.Context) and hasattr(e, "set_planar_prior_from_state")
 
     def _state_buffers(self, ref, shape):
         """The HBM copy of view `ref`'s last planes and costs: one allocation per view, sized for its

@@ -104,6 +104,8 @@ struct acmmp_ctx {
     bool has_prior = false;           // set_planar_prior since the last upload_views
     char* d_pp = nullptr;             // planar-prior triangle tables (acmmp_set_planar_prior_from_maps)
     size_t pp_cap = 0;
+    int4* d_support = nullptr;        // support-point blocks (acmmp_set_planar_prior_from_state)
+    size_t support_cap = 0;
 
     float4* d_plane_cs[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
     float* d_cost_cs[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
@@ -287,7 +289,7 @@ void acmmp_destroy(acmmp_ctx* c) {
     dfree(c->d_stage); dfree(c->d_flag);
     dfree(c->d_sph_row); dfree(c->d_sph_col); dfree(c->d_spatial);
     dfree(c->d_planes_rm); dfree(c->d_costs_rm); dfree(c->d_pre); dfree(c->d_sel_rm);
-    dfree(c->d_scaled); dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_pp); dfree(c->d_scratch); dfree(c->d_work);
+    dfree(c->d_scaled); dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_pp); dfree(c->d_support); dfree(c->d_scratch); dfree(c->d_work);
     for (int k = 0; k < 2; ++k) {
         for (int b = 0; b < 2; ++b) { dfree(c->d_plane_cs[k][b]); dfree(c->d_cost_cs[k][b]); }
         dfree(c->d_sel_cs[k]); dfree(c->d_rng_cs[k]);
@@ -767,17 +769,13 @@ acmmp_status acmmp_set_planar_prior(acmmp_ctx* c, const float* prior, const uint
     return ACMMP_OK;
 }
 
-acmmp_status acmmp_set_planar_prior_from_maps(acmmp_ctx* c, const float* depths, const float* costs, float depth_min,
-                                              float depth_max, int* n_triangles) {
-    if (!c || !depths || !costs) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
-    if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
-    HIP_TRY(c, hipSetDevice(c->device));
+// The device half of the planar block for host-computed triangles: one upload of the tables, the raster
+// and the prior-depth mask / expansion kernels, into the context's planar-prior state.
+static acmmp_status upload_planar(acmmp_ctx* c, const PlanarTriangles& pt, float depth_min, float depth_max,
+                                  int* n_triangles) {
     const acmmp_camera& cam = c->cams[0];
     const int W = c->W, H = c->H;
     const size_t P = P_of(c);
-    PlanarTriangles pt;
-    const acmmp_status st = planar_triangles(cam, depths, costs, W, H, &pt);
-    if (st != ACMMP_OK) return fail(c, st, "planar_triangles");
     const int m = static_cast<int>(pt.step.size());
     // one upload: first[] (8 B aligned) | plane (float4) | tri | step | row/col trig
     auto up = [](size_t b) { return (b + 255) & ~static_cast<size_t>(255); };
@@ -818,6 +816,44 @@ acmmp_status acmmp_set_planar_prior_from_maps(acmmp_ctx* c, const float* depths,
     c->has_prior = true;
     if (n_triangles) *n_triangles = m;
     return ACMMP_OK;
+}
+
+acmmp_status acmmp_set_planar_prior_from_maps(acmmp_ctx* c, const float* depths, const float* costs, float depth_min,
+                                              float depth_max, int* n_triangles) {
+    if (!c || !depths || !costs) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
+    if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    PlanarTriangles pt;
+    const acmmp_status st = planar_triangles(c->cams[0], depths, costs, c->W, c->H, &pt);
+    if (st != ACMMP_OK) return fail(c, st, "planar_triangles");
+    return upload_planar(c, pt, depth_min, depth_max, n_triangles);
+}
+
+acmmp_status acmmp_set_planar_prior_from_state(acmmp_ctx* c, float depth_min, float depth_max, int* n_triangles) {
+    if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
+    if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views and run_patchmatch first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const int W = c->W, H = c->H;
+    const size_t nb = static_cast<size_t>((W + 4) / 5) * ((H + 4) / 5);
+    HIP_TRY(c, dreserve(c->d_support, c->support_cap, nb));
+    HIP_TRY(c, launch_support_points(c->d_costs_rm, c->d_planes_rm, W, H, c->d_support, c->stream));
+    std::vector<int4> blocks(nb);
+    HIP_TRY(c, hipMemcpyAsync(blocks.data(), c->d_support, sizeof(int4) * nb, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<int> xy;
+    std::vector<float> depth_at;
+    for (const int4& b : blocks) {                          // the reference's order: strip-major
+        if (!b.x) continue;
+        xy.push_back(b.y);
+        xy.push_back(b.z);
+        float d;
+        std::memcpy(&d, &b.w, sizeof d);
+        depth_at.push_back(d);
+    }
+    PlanarTriangles pt;
+    const acmmp_status st = planar_triangles_pts(c->cams[0], xy, depth_at, W, H, &pt);
+    if (st != ACMMP_OK) return fail(c, st, "planar_triangles");
+    return upload_planar(c, pt, depth_min, depth_max, n_triangles);
 }
 
 acmmp_status acmmp_download_planar_prior(acmmp_ctx* c, float* prior, uint32_t* masks) {

@@ -936,39 +936,65 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     // (Get3DPointonWorld_cu's pinhole branch, ACMMP.cu:579-581) and depth_s = -w / D_s, D_s = n . r_s for the
     // normalised table ray r_s (ACMMP.cu:187-193); its source image point FR (depth_s v_s) + Ft, scaled by
     // w / depth_s (a projective scale: the same x / z and y / z), is
-    //     w FR v_s - D_s Ft,     FR v_s = FR v_0 + i FR e_x / fx + j FR e_y / fy,
-    // affine in (i, j).  So per view the lane forms h0 = w FR v_0 and the steps hi = w FR e_x / fx,
-    // hj = w FR e_y / fy once per chunk, and per sample fma(j, hj, fma(i, hi, h0)) - D_s Ft: 4 VALU per
-    // view-sample for the point (project_fast: 6 plus 2 moves of Ft, plus the depth division and the point
-    // per sample), and no FR in scalar registers across the loop (at 4 views they spilled).  The
-    // reference's depth clamp (|D_s| < 1e-6: depth 1e6) is the scale w * 1e-6 in place of -D_s.
+    //     h(i, j) = w FR v_s + S_s Ft,   S_s = -D_s (w 1e-6 where |D_s| < 1e-6: the reference's depth 1e6),
+    // and w FR v_s = w FR v_0 + i w FR e_x / fx + j w FR e_y / fy is affine in (i, j).  It is taken relative
+    // to the pixel's own source point (X0, Y0) = h_c.xy / h_c.z, h_c = h(0, 0) formed in binary64 from the
+    // binary32 inputs: x(i, j) = X0 + N_x / h_z with N_x = h_x - X0 h_z affine in (i, j) and S_s - S_c, all its
+    // terms small -- so the per-sample arithmetic rounds at the scale of the patch's pixel offsets, not of
+    // the image coordinates.  Per view-sample 6 VALU for the point (project_fast: 8 plus 2 moves of Ft, plus
+    // the depth division and the point per sample) and no FR in scalar registers across the loop; in
+    // binary32 emulation (C5 / C2 cameras, near-surface planes) the coordinates are ~2x closer to float64
+    // than the per-sample form's (q99 8e-5 vs 1.7e-4 px).
     constexpr bool kHomog = FM && MODEL == kPinhole && STAGED == 3;
     if constexpr (kHomog) if (kp.homog) {
         interp_done = true;
         ConstCam& c0 = ccams[0];
         const float v0x = (static_cast<float>(px) - c0.K[2]) * c0.inv_fx;
         const float v0y = (static_cast<float>(py) - c0.K[5]) * c0.inv_fy;
-        float h0[VB][3], hi[VB][3], hj[VB][3];
+        const float w_clamp = ph.w * 1e-6f;
+        const float D0 = dot3(ph.x, ph.y, ph.z, dc.x, dc.y, dc.z);
+        const float s0 = fabsf(D0) < 1e-6f ? w_clamp : -D0;
+        // per view: N = (N0 + i hi' + j hj' + dS Ft') relative to (X0, Y0), z = hz + i hi.z + j hj.z + dS Ft.z
+        f32x2 n0[VB], hi2[VB], hj2[VB], ft2[VB], xy0[VB];
+        float z0[VB], hiz[VB], hjz[VB];
 #pragma unroll
         for (int v = 0; v < VB; ++v) {
+            n0[v] = hi2[v] = hj2[v] = ft2[v] = xy0[v] = splat2(0.f);
+            z0[v] = hiz[v] = hjz[v] = 0.f;
+            if (has(v)) {
+                ConstCam& c = PCV(v);
+                double hc[3];
+                float hi[3], hj[3];
 #pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                h0[v][r] = hi[v][r] = hj[v][r] = 0.f;
-                if (has(v)) {
-                    ConstCam& c = PCV(v);
+                for (int r = 0; r < 3; ++r) {
                     const float f0 = r < 2 ? c.FRxy[r] : c.FRz[0];        // FR[r][0]
                     const float f1 = r < 2 ? c.FRxy[2 + r] : c.FRz[1];    // FR[r][1]
                     const float f2 = r < 2 ? c.FRxy[4 + r] : c.FRz[2];    // FR[r][2]
-                    h0[v][r] = ph.w * fmaf(f1, v0y, fmaf(f0, v0x, f2));
-                    hi[v][r] = ph.w * (f0 * c0.inv_fx);
-                    hj[v][r] = ph.w * (f1 * c0.inv_fy);
+                    const double g = fma(static_cast<double>(f1), static_cast<double>(v0y),
+                                         fma(static_cast<double>(f0), static_cast<double>(v0x), static_cast<double>(f2)));
+                    hc[r] = fma(static_cast<double>(s0), static_cast<double>(c.Ft[r]), static_cast<double>(ph.w) * g);
+                    hi[r] = ph.w * (f0 * c0.inv_fx);
+                    hj[r] = ph.w * (f1 * c0.inv_fy);
                 }
+                const float hz = static_cast<float>(hc[2]);
+                const float rz = __builtin_amdgcn_rcpf(hz);
+                const float X0 = static_cast<float>(hc[0]) * rz, Y0 = static_cast<float>(hc[1]) * rz;
+                xy0[v] = (f32x2){X0, Y0};
+                n0[v] = (f32x2){static_cast<float>(fma(-static_cast<double>(X0), hc[2], hc[0])),
+                                static_cast<float>(fma(-static_cast<double>(Y0), hc[2], hc[1]))};
+                hi2[v] = (f32x2){fmaf(-X0, hi[2], hi[0]), fmaf(-Y0, hi[2], hi[1])};
+                hj2[v] = (f32x2){fmaf(-X0, hj[2], hj[0]), fmaf(-Y0, hj[2], hj[1])};
+                ft2[v] = (f32x2){fmaf(-X0, c.Ft[2], c.Ft[0]), fmaf(-Y0, c.Ft[2], c.Ft[1])};
+                z0[v] = hz;
+                hiz[v] = hi[2];
+                hjz[v] = hj[2];
             }
         }
         // each view's image descriptor and bounds formed once, before the loop (built at their use, the
         // compiler re-read their fields through scalar loads per sample)
         __amdgpu_buffer_rsrc_t rsv[VB];
         int wm1[VB], hm1[VB], p4[VB];
+        float ftz[VB];
 #pragma unroll
         for (int v = 0; v < VB; ++v) {
             ConstCam& c = PCV(v);
@@ -978,22 +1004,24 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             wm1[v] = uniform_int(c.Wm1);
             hm1[v] = uniform_int(c.Hm1);
             p4[v] = uniform_int(c.pitch4);
+            ftz[v] = c.Ft[2];
         }
-        const float w_clamp = ph.w * 1e-6f;
         int s = 0;
         for (int i = -R; i <= R; i += inc) {
             const float fi = static_cast<float>(i);
-            float hr[VB][3];
+            f32x2 nr[VB];
+            float zr[VB];
 #pragma unroll
-            for (int v = 0; v < VB; ++v)
-#pragma unroll
-                for (int r = 0; r < 3; ++r) hr[v][r] = fmaf(fi, hi[v][r], h0[v][r]);
+            for (int v = 0; v < VB; ++v) {
+                nr[v] = pk_fma(splat2(fi), hi2[v], n0[v]);
+                zr[v] = fmaf(fi, hiz[v], z0[v]);
+            }
             for (int j = -R; j <= R; j += inc, ++s) {
                 const float fj = static_cast<float>(j);
                 const float4 q = pt.rw[s * pt.stride];      // (r_s, w_s)
                 const float r = pt.rr[s * pt.stride];
                 const float D = dot3(ph.x, ph.y, ph.z, q.x, q.y, q.z);
-                const float sc = fabsf(D) < 1e-6f ? w_clamp : -D;
+                const float dS = (fabsf(D) < 1e-6f ? w_clamp : -D) - s0;
                 const float w = q.w;
                 const f32x2 wwr = (f32x2){w, w * r};
                 Tap tap[VB];
@@ -1002,12 +1030,11 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 for (int v = 0; v < VB; ++v) {
                     ok[v] = false;
                     if (has(v)) {
-                        ConstCam& c = PCV(v);
-                        f32x2 t = pk_fma(splat2(fj), (f32x2){hj[v][0], hj[v][1]}, (f32x2){hr[v][0], hr[v][1]});
-                        float tz = fmaf(fj, hj[v][2], hr[v][2]);
-                        t = pk_fma(splat2(sc), (f32x2){c.Ft[0], c.Ft[1]}, t);
-                        tz = fmaf(sc, c.Ft[2], tz);
-                        const f32x2 o = t * splat2(__builtin_amdgcn_rcpf(tz));
+                        f32x2 nn = pk_fma(splat2(fj), hj2[v], nr[v]);
+                        float tz = fmaf(fj, hjz[v], zr[v]);
+                        nn = pk_fma(splat2(dS), ft2[v], nn);
+                        tz = fmaf(dS, ftz[v], tz);
+                        const f32x2 o = pk_fma(nn, splat2(__builtin_amdgcn_rcpf(tz)), xy0[v]);
                         const int ix = cvt_flr_i32(o.x), iy = cvt_flr_i32(o.y);
                         ok[v] = (static_cast<unsigned>(ix) <= static_cast<unsigned>(wm1[v])) &
                                 (static_cast<unsigned>(iy) <= static_cast<unsigned>(hm1[v]));   // pin_in_image
@@ -1659,7 +1686,7 @@ constexpr bool kNbPipeExact = false, kNbPipeFast = true;
 // fast pinhole chunks (the homogeneous sample points of ncc_chunk): views per chunk (ACMMP_NB_PIN_VB
 // overrides at build time for A/B builds)
 #ifndef ACMMP_NB_PIN_VB
-#define ACMMP_NB_PIN_VB 4
+#define ACMMP_NB_PIN_VB 2
 #endif
 template <int MODEL, int VB, int FM>
 constexpr int nb_vb() {
@@ -2910,6 +2937,36 @@ hipError_t launch_planar_raster(const PlanarDev& pd, uint32_t* mask, hipStream_t
 
 hipError_t launch_planar_mask(const PlanarDev& pd, uint32_t* mask, float4* prior, hipStream_t s) {
     k_planar_mask<<<dim3(cdiv(pd.W, 256), pd.H), 256, 0, s>>>(pd, mask, prior);
+    return hipGetLastError();
+}
+
+// GetSupportPoints (ACMMP.cpp:904-929) on the context's last RunPatchMatch output: one thread per 5x5
+// block, scanned column by column with the reference's strict '>' (the first minimum-cost pixel, costs
+// 2.0 and above skipped), kept when the minimum is < 0.1.  out[strip * bh + block row] = (kept, x, y,
+// depth bits) -- the reference's point order is strip-major, block rows within a strip.
+__global__ __launch_bounds__(256) void k_support_points(const float* __restrict__ costs, const float4* __restrict__ planes,
+                                                        int W, int H, int bh, int4* __restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int bw = (W + 4) / 5;
+    if (t >= bw * bh) return;
+    const int strip = t / bh, rb = t - strip * bh;
+    const int col = strip * 5, row = rb * 5;
+    const int cb = min(W, col + 5), rbe = min(H, row + 5);
+    float min_cost = 2.0f;
+    int tx = 0, ty = 0;
+    for (int c = col; c < cb; ++c)
+        for (int r = row; r < rbe; ++r) {
+            const float v = costs[static_cast<long long>(r) * W + c];
+            if (v < 2.0f && min_cost > v) { tx = c; ty = r; min_cost = v; }
+        }
+    const bool keep = min_cost < 0.1f;
+    const float d = keep ? planes[static_cast<long long>(ty) * W + tx].w : 0.0f;
+    out[t] = make_int4(keep ? 1 : 0, tx, ty, __float_as_int(d));
+}
+
+hipError_t launch_support_points(const float* costs, const float4* planes, int W, int H, int4* out, hipStream_t s) {
+    const int bh = (H + 4) / 5, n = ((W + 4) / 5) * bh;
+    k_support_points<<<cdiv(n, 256), 256, 0, s>>>(costs, planes, W, H, bh, out);
     return hipGetLastError();
 }
 

@@ -26,6 +26,10 @@ struct PlanarTriangles {
 // Host half: support points of `costs`, Delaunay, labelled triangles, their planes through `depths`.
 acmmp_status planar_triangles(const acmmp_camera& cam, const float* depths, const float* costs, int W, int H,
                               PlanarTriangles* out);
+// The same from support points found elsewhere (xy: 2 ints per point in the reference's order) and the
+// depth at each point.
+acmmp_status planar_triangles_pts(const acmmp_camera& cam, const std::vector<int>& xy,
+                                  const std::vector<float>& depth_at, int W, int H, PlanarTriangles* out);
 
 // Device half (kernels.hip).  mask: P uint32 zeroed by the caller; prior: P float4.
 struct PlanarDev {
@@ -43,5 +47,8 @@ struct PlanarDev {
 };
 hipError_t launch_planar_raster(const PlanarDev& pd, uint32_t* mask, hipStream_t s);
 hipError_t launch_planar_mask(const PlanarDev& pd, uint32_t* mask, float4* prior, hipStream_t s);
+// GetSupportPoints on device maps (costs, planes' .w = depth, row-major W x H): ((W + 4) / 5) * ((H + 4) / 5)
+// int4 (kept, x, y, depth bits), strip-major.
+hipError_t launch_support_points(const float* costs, const float4* planes, int W, int H, int4* out, hipStream_t s);
 
 }  // namespace acmmp

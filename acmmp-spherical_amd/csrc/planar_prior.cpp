@@ -331,6 +331,23 @@ float sphere_depth(const float plane[4], SphereTrig lat, SphereTrig lon) {
     return (std::abs(denom) < 1e-6f) ? 1e6f : (-plane[3] / denom);
 }
 
+// GetPriorPlaneParams (ACMMP.cpp:957-989) through the three vertices' depths d3
+void prior_plane(const acmmp_camera& cam, const int tri_xy[6], const float d3[3], float plane[4]) {
+    float X[3][3];
+    for (int k = 0; k < 3; ++k) point_on_ref_cam(tri_xy[2 * k], tri_xy[2 * k + 1], d3[k], cam, X[k]);
+
+    // cv::SVD::solveZ on [X_k 1] (3x4): the null vector, i.e. the plane through the three points
+    // (ACMMP.cpp:960-980).  Closed form (SURVEY.md §8a a15): n = (X2-X1) x (X3-X1), w = -n.X1.
+    const float e1[3] = {X[1][0] - X[0][0], X[1][1] - X[0][1], X[1][2] - X[0][2]};
+    const float e2[3] = {X[2][0] - X[0][0], X[2][1] - X[0][1], X[2][2] - X[0][2]};
+    float n4[4] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0], 0.f};
+    n4[3] = -(n4[0] * X[0][0] + n4[1] * X[0][1] + n4[2] * X[0][2]);
+    // ACMMP.cpp:981-988: normalise by the normal's length, sign so that w >= 0
+    float norm2 = static_cast<float>(std::sqrt(std::pow(n4[0], 2) + std::pow(n4[1], 2) + std::pow(n4[2], 2)));
+    if (n4[3] < 0) norm2 *= -1;
+    for (int k = 0; k < 4; ++k) plane[k] = n4[k] / norm2;
+}
+
 }  // namespace
 
 extern "C" {
@@ -366,22 +383,13 @@ acmmp_status acmmp_delaunay(const int* xy, int n, int W, int H, int* tri_xy, int
 acmmp_status acmmp_prior_plane_params(const acmmp_camera* cam, const float* depths, int W, int H, const int tri_xy[6],
                                       float plane[4]) {
     if (!cam || !depths || !tri_xy || !plane || W <= 0 || H <= 0) return ACMMP_ERR_INVALID_ARGUMENT;
-    float X[3][3];
+    float d3[3];
     for (int k = 0; k < 3; ++k) {
         const int x = tri_xy[2 * k], y = tri_xy[2 * k + 1];
         if (x < 0 || x >= W || y < 0 || y >= H) return ACMMP_ERR_INVALID_ARGUMENT;
-        point_on_ref_cam(x, y, depths[static_cast<size_t>(y) * W + x], *cam, X[k]);
+        d3[k] = depths[static_cast<size_t>(y) * W + x];
     }
-    // cv::SVD::solveZ on [X_k 1] (3x4): the null vector, i.e. the plane through the three points
-    // (ACMMP.cpp:960-980).  Closed form (SURVEY.md §8a a15): n = (X2-X1) x (X3-X1), w = -n.X1.
-    const float e1[3] = {X[1][0] - X[0][0], X[1][1] - X[0][1], X[1][2] - X[0][2]};
-    const float e2[3] = {X[2][0] - X[0][0], X[2][1] - X[0][1], X[2][2] - X[0][2]};
-    float n4[4] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0], 0.f};
-    n4[3] = -(n4[0] * X[0][0] + n4[1] * X[0][1] + n4[2] * X[0][2]);
-    // ACMMP.cpp:981-988: normalise by the normal's length, sign so that w >= 0
-    float norm2 = static_cast<float>(std::sqrt(std::pow(n4[0], 2) + std::pow(n4[1], 2) + std::pow(n4[2], 2)));
-    if (n4[3] < 0) norm2 *= -1;
-    for (int k = 0; k < 4; ++k) plane[k] = n4[k] / norm2;
+    prior_plane(*cam, tri_xy, d3, plane);
     return ACMMP_OK;
 }
 
@@ -459,8 +467,16 @@ namespace acmmp {
 acmmp_status planar_triangles(const acmmp_camera& cam, const float* depths, const float* costs, int W, int H,
                               PlanarTriangles* out) {
     const std::vector<int> xy = support_points(costs, W, H);
+    std::vector<float> depth_at(xy.size() / 2);
+    for (size_t i = 0; i < depth_at.size(); ++i)
+        depth_at[i] = depths[static_cast<size_t>(xy[2 * i + 1]) * W + xy[2 * i]];
+    return planar_triangles_pts(cam, xy, depth_at, W, H, out);
+}
+
+acmmp_status planar_triangles_pts(const acmmp_camera& cam, const std::vector<int>& xy,
+                                  const std::vector<float>& depth_at, int W, int H, PlanarTriangles* out) {
     const int n = static_cast<int>(xy.size() / 2);
-    std::vector<int> tri;
+    std::vector<int> tri, tri_pt;                          // vertex coordinates / point indices
     if (n > 0) {                                           // triangulate once (ACMMP.cpp:932-955)
         std::vector<Pt> pts(n);
         for (int i = 0; i < n; ++i) pts[i] = {xy[2 * i], xy[2 * i + 1]};
@@ -473,7 +489,11 @@ acmmp_status planar_triangles(const acmmp_camera& cam, const float* depths, cons
                 inside = inside && x >= 0 && x < W && y >= 0 && y < H;
             }
             if (!inside) continue;
-            for (int j = 0; j < 3; ++j) { tri.push_back(xy[2 * t[j]]); tri.push_back(xy[2 * t[j] + 1]); }
+            for (int j = 0; j < 3; ++j) {
+                tri.push_back(xy[2 * t[j]]);
+                tri.push_back(xy[2 * t[j] + 1]);
+                tri_pt.push_back(t[j]);
+            }
         }
     }
     const int m = static_cast<int>(tri.size() / 6);
@@ -492,7 +512,8 @@ acmmp_status planar_triangles(const acmmp_camera& cam, const float* depths, cons
         long long c = 0;
         for (float p = 0; p < 1.0; p += step) ++c;
         np[k] = c;
-        acmmp_prior_plane_params(&cam, depths, W, H, t, &out->plane[4 * static_cast<size_t>(k)]);
+        const float d3[3] = {depth_at[tri_pt[3 * k]], depth_at[tri_pt[3 * k + 1]], depth_at[tri_pt[3 * k + 2]]};
+        prior_plane(cam, t, d3, &out->plane[4 * static_cast<size_t>(k)]);
     });
     out->first.assign(static_cast<size_t>(m) + 1, 0);
     for (int k = 0; k < m; ++k) out->first[k + 1] = out->first[k] + np[k];

@@ -70,6 +70,18 @@ def eval_nb_executed_flop_per_pixel(V: int) -> float:
     return 8 * V * F_INTERP_VIEW + 36 * 30.0
 
 
+# What the fast pinhole k_eval_nb executes per hypothesis-view-sample with the centre-relative homogeneous
+# sample points: the point 8 FMA + the perspective reciprocal (16 + 3, in place of SURVEY.md
+# §8d's 24 + 3), the row step 1, bilinear 13, accumulation 6 -- 39 of F_HVS's 46; per sample the ray-plane
+# dot and the scale step 6 (in place of 15); per hypothesis-view the binary64 centre point and the relative
+# rows, ~60.
+F_HOMOG_HVS, F_HOMOG_SAMPLE, F_HOMOG_VIEW = 39.0, 6.0, 60.0
+
+
+def eval_nb_executed_flop_per_pixel_pinhole(V: int, samples: int = 36) -> float:
+    return 8 * (samples * (V * F_HOMOG_HVS + F_HOMOG_SAMPLE) + V * F_HOMOG_VIEW) + samples * 30.0
+
+
 def interp_enabled(width: int, height: int, patch_size: int = 11, radius_increment: int = 2) -> bool:
     """capi.cpp build_kparams' gate (tests/np_interp.interp_enabled)."""
     R = patch_size // 2
@@ -676,6 +688,11 @@ def main():
         ex_tf = ex_flop / (launch_ms * 1e-3) / 1e12
         executed = {"flop_per_launch": ex_flop, "achieved": round(ex_tf, 3), "frac": round(ex_tf / PEAK_FP32_TFLOPS, 4),
                     "note": "16 projected + 20 interpolated samples per hypothesis-view (bench.F_INTERP_VIEW)"}
+    elif args.math == "fast" and args.model == "pinhole" and os.environ.get("ACMMP_PIN_HOMOG", "1") != "0":
+        ex_flop = eval_nb_executed_flop_per_pixel_pinhole(args.n_src) * pix_per_launch
+        ex_tf = ex_flop / (launch_ms * 1e-3) / 1e12
+        executed = {"flop_per_launch": ex_flop, "achieved": round(ex_tf, 3), "frac": round(ex_tf / PEAK_FP32_TFLOPS, 4),
+                    "note": "centre-relative homogeneous sample points (bench.F_HOMOG_*)"}
     roofline = {
         "bound": "valu",
         "achieved": round(achieved, 3),

@@ -338,6 +338,13 @@ acmmp_status acmmp_planar_prior_host(const acmmp_camera *cam0, const float *dept
  * 20 B/pixel upload.  No reference counterpart. */
 acmmp_status acmmp_set_planar_prior_from_maps(acmmp_ctx *ctx, const float *depths, const float *costs,
                                               float depth_min, float depth_max, int *n_triangles);
+/* The same planar block from the context's own last RunPatchMatch output in HBM (main.cpp:113-181 runs
+ * it on the first run's depths and costs): GetSupportPoints (ACMMP.cpp:904-929) on the device, only the
+ * support points (and their depths) to the host for the Delaunay triangulation and the per-triangle planes,
+ * then the raster / mask / expansion of acmmp_set_planar_prior_from_maps.  Equal to
+ * acmmp_set_planar_prior_from_maps on the downloaded maps, bit for bit (tests/test_gpu_planar_state.py);
+ * no full-map download. */
+acmmp_status acmmp_set_planar_prior_from_state(acmmp_ctx *ctx, float depth_min, float depth_max, int *n_triangles);
 /* Test hook: the planar-prior state of the context (P float4 planes, P labels; either may be NULL). */
 acmmp_status acmmp_download_planar_prior(acmmp_ctx *ctx, float *prior_planes, uint32_t *masks);
 

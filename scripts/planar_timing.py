@@ -1,5 +1,5 @@
 """Host planar-prior stage timing on a real first-pass RunPatchMatch output (GPU box): support points,
-Delaunay, the full host block, and the device path (acmmp_set_planar_prior_from_maps)."""
+Delaunay, the full host block, and the device paths (acmmp_set_planar_prior_from_maps / _from_state)."""
 import json
 import os
 import sys
@@ -37,4 +37,9 @@ for _ in range(3):
     t = time.perf_counter(); ctx.set_planar_prior_from_maps(depth, costs, float(p["depth_min"]), float(p["depth_max"]))
     ts.append((time.perf_counter() - t) * 1e3)
 out["set_planar_prior_from_maps_ms"] = ts
+ts = []
+for _ in range(3):
+    t = time.perf_counter(); out["n_tri_state"] = ctx.set_planar_prior_from_state(float(p["depth_min"]), float(p["depth_max"]))
+    ts.append((time.perf_counter() - t) * 1e3)
+out["set_planar_prior_from_state_ms"] = ts
 print(json.dumps(out))

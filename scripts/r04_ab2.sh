@@ -1,12 +1,12 @@
 #!/bin/bash
 # Round-4 A/B of the working tree (GPU box, repo root): fast-mode / per-query tests (reports), the GPU suite,
 # then bench lines -- metric with the deferred interpolation fallbacks (product) and inline (ACMMP_NB_FIX=0),
-# metric exact, C3 fast / exact (dense XCD-segment refinement tail), C2 with the homogeneous pinhole points
-# on / off at 4- and 2-view chunks -- and the planar-prior host timing.  Usage: bash scripts/r04_ab2.sh TAG
+# metric exact, C3 fast / exact (dense XCD-segment refinement tail), C2 with the centre-relative homogeneous
+# pinhole points on / off (2-view chunks) and round 3's per-sample 4-view chunks -- and the planar-prior timing.  Usage: bash scripts/r04_ab2.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r04_ab2}
-V2=acmmp-spherical_amd/acmmp/libacmmp_pinvb2.so
+V4=acmmp-spherical_amd/acmmp/libacmmp_pinvb4.so
 mkdir -p $OUT
 export ACMMP_TEST_REPORT_DIR=$OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_interp.py tests/test_gpu_fastmath.py -v -rA --timeout 300 --timeout-method thread > $OUT/pytest_fast.log 2>&1
@@ -34,10 +34,9 @@ line metric_exact timeout -k 10 300 python bench.py $Q --math exact
 line c3 timeout -k 10 400 python bench.py $C3 $Q
 line c3_exact timeout -k 10 400 python bench.py $C3 $Q --math exact
 for rep in 1 2; do
-  line c2_homog4 timeout -k 10 300 python bench.py $C2 $Q
-  line c2_sample4 ACMMP_PIN_HOMOG=0 timeout -k 10 300 python bench.py $C2 $Q
-  line c2_homog2 ACMMP_LIB=$V2 timeout -k 10 300 python bench.py $C2 $Q
-  line c2_sample2 ACMMP_LIB=$V2 ACMMP_PIN_HOMOG=0 timeout -k 10 300 python bench.py $C2 $Q
+  line c2_homog2 timeout -k 10 300 python bench.py $C2 $Q
+  line c2_sample2 ACMMP_PIN_HOMOG=0 timeout -k 10 300 python bench.py $C2 $Q
+  line c2_sample4 ACMMP_LIB=$V4 ACMMP_PIN_HOMOG=0 timeout -k 10 300 python bench.py $C2 $Q
 done
 timeout -k 10 300 python scripts/planar_timing.py 2000 1500 sphere > $OUT/planar_2000x1500_sphere.json 2> $OUT/planar.err || { echo "planar timing failed"; tail -5 $OUT/planar.err; exit 1; }
 timeout -k 10 300 python scripts/planar_timing.py 1600 1200 pinhole > $OUT/planar_1600x1200_pinhole.json 2>> $OUT/planar.err || { echo "planar timing failed"; tail -5 $OUT/planar.err; exit 1; }
