@@ -914,12 +914,12 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.W = c->W; kp.H = c->H; kp.Wh = Wh_of(c); kp.N = c->N; kp.V = c->N - 1;
     kp.R = R; kp.inc = p.radius_increment; kp.nside = nside; kp.S = nside * nside;
     // interpolated SPHERE sample coordinates in the fast k_eval_nb: 6x6 patches whose
-    // radius spans at most 5 pixels of 2 pi / 1600 rad (the geometry the float64 study validated:
-    // patch_size 11, radius_increment 2 from 1600x800 up) -- a wider patch angle makes the interpolation's
-    // NCC error exceed 1e-4 in the tail (scripts/interp_feasibility.py; at 1600x800 the largest error is
-    // 6.7e-5, at 1280x640, R = 5 spanning 1.25x the angle, 8.5e-3).  patch_size 21 / increment 4 also
-    // gives 6x6 samples but spans twice the angle: it projects every sample below 3200x1600.
-    kp.interp = c->model == kSphere && nside == 6 && 1600LL * R <= 5LL * c->W && 800LL * R <= 5LL * c->H;
+    // radius spans at most 5 pixels of 2 pi / 2000 rad (patch_size 11, radius_increment 2 from 2000x1000
+    // up) -- a wider patch angle makes the interpolation's NCC error exceed 1e-4 in the tail near source
+    // poles, where the 256-pixel corner-spread fallback no longer catches it (1600x800: 3.7e-3 at a spread
+    // of 65 px; scripts/interp_feasibility.py, tests/test_interp_design.py).  patch_size 21 / increment 4
+    // also gives 6x6 samples but spans twice the angle: it projects every sample below 4000x2000.
+    kp.interp = c->model == kSphere && nside == 6 && 2000LL * R <= 5LL * c->W && 1000LL * R <= 5LL * c->H;
     // ACMMP_INTERP=0 projects every sample in the fast mode too (the per-sample fast arithmetic the
     // interpolation is gated against, tests/test_gpu_fastmath.py T2); read per run
     if (const char* e = std::getenv("ACMMP_INTERP")) kp.interp = kp.interp && std::atoi(e) != 0;
@@ -927,6 +927,10 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     // ACMMP_PIN_HOMOG=0 projects it through depth and point per sample instead (A/B, tests)
     kp.homog = 1;
     if (const char* e = std::getenv("ACMMP_PIN_HOMOG")) kp.homog = std::atoi(e) != 0;
+    // the interpolation's corner-spread fallback threshold (ncc_chunk); ACMMP_SPREAD_MAX overrides it (tests
+    // force fallbacks with a small one, A/B without any with a huge one)
+    kp.spread_max = 256.0f;
+    if (const char* e = std::getenv("ACMMP_SPREAD_MAX")) kp.spread_max = std::strtof(e, nullptr);
     kp.rows = std::min(c->H, 32 * (((c->H / 2) + 15) / 16));
     kp.row_lo = 0; kp.row_hi = kp.rows;
     kp.init_lo = 0; kp.init_hi = c->H;
@@ -961,22 +965,23 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     HIP_TRY(c, dreserve(c->d_spatial, c->spatial_cap, static_cast<size_t>(c->model == kSphere ? c->H : 1) * kp.S));
     HIP_TRY(c, launch_spatial_table(kp, c->d_spatial, c->stream));
     // half-sweep scratch slab: carve the pieces of engine.h's KParams out of one allocation
-    size_t off[16];
+    size_t off[17];
     {
         const size_t VP = static_cast<size_t>(kp.V) * Pc;
-        const size_t sizes[15] = {sizeof(float) * 8 * VP, sizeof(int) * 8 * Pc,
+        const size_t sizes[16] = {sizeof(float) * 8 * VP, sizeof(int) * 8 * Pc,
                                   sizeof(float4) * 5 * Pc, sizeof(float) * 5 * Pc, sizeof(float) * 5 * Pc,
                                   sizeof(PixState) * Pc, sizeof(float) * VP, sizeof(float) * VP,
                                   sizeof(float) * 5 * VP, sizeof(uint32_t) * (5 * Pc + 256),
                                   sizeof(unsigned) * (Pc / 51 + 2),
-                                  sizeof(float4) * Pc, sizeof(uint32_t) * kNbFixPerPixel * Pc, sizeof(unsigned),
-                                  sizeof(unsigned) * (Pc / 51 + 3)};
+                                  sizeof(float4) * Pc, sizeof(uint32_t) * kNbFixPerPixel * Pc + 1024,
+                                  sizeof(unsigned) * kNbFixRegions,
+                                  sizeof(unsigned) * (Pc / 51 + 3), sizeof(uint32_t) * (5 * Pc + 256)};
         off[0] = 0;
-        for (int k = 0; k < 15; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
+        for (int k = 0; k < 16; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
     }
-    if (c->scratch_bytes < off[15]) {
-        HIP_TRY(c, dalloc(c->d_scratch, off[15]));
-        c->scratch_bytes = off[15];
+    if (c->scratch_bytes < off[16]) {
+        HIP_TRY(c, dalloc(c->d_scratch, off[16]));
+        c->scratch_bytes = off[16];
     }
     kp.cams = c->d_cams;
     kp.tex16 = c->tex16;
@@ -1013,7 +1018,8 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.nbfix = fixq ? reinterpret_cast<uint32_t*>(c->d_scratch + off[12]) : nullptr;
     kp.nbfix_count = reinterpret_cast<unsigned*>(c->d_scratch + off[13]);
     kp.surv_pre = reinterpret_cast<unsigned*>(c->d_scratch + off[14]);
-    kp.nbfix_cap = fixq ? static_cast<unsigned>(kNbFixPerPixel * Pc) : 0u;
+    kp.surv_dense = reinterpret_cast<uint32_t*>(c->d_scratch + off[15]);
+    kp.nbfix_cap = fixq ? static_cast<unsigned>(kNbFixPerPixel * Pc / kNbFixRegions) : 0u;
     kp.ref_split = ref_split_point(kp.V, Pc);
     if (!c->d_work) HIP_TRY(c, dalloc(c->d_work, 256));
     kp.work = c->d_work;

@@ -27,6 +27,7 @@ constexpr int kPinhole = 0;
 constexpr int kSphere = 11;
 constexpr int kMaxViews = 32;       // cost_vector[32], uint32 view bitmask (ACMMP.cu:522,1153)
 constexpr int kNbFixPerPixel = 8;   // queue entries per colour-grid pixel for k_eval_nb's deferred fallbacks
+constexpr int kNbFixRegions = 256;  // the queue's regions, one counter each (block % regions)
 
 struct DevCam {
     // The fields the fast-math sample loop reads come first, contiguous and 16-byte aligned, so each
@@ -85,6 +86,7 @@ struct KParams {
     int R, inc, nside, S;           // patch radius, radius_increment, offsets per axis, samples
     int interp;                     // fast SPHERE k_eval_nb interpolates sample coordinates
     int homog;                      // fast pinhole staged chunks: homogeneous sample points
+    float spread_max;               // interpolation fallback threshold, source pixels (ACMMP_SPREAD_MAX, 256)
     int rows;                       // rows the reference's checkerboard grid covers
     // row ranges (full image by default; a row band in the split latency mode, acmmp_band_*):
     int row_lo, row_hi;             // colour-grid rows the half-sweep kernels update, within [0, rows)
@@ -137,12 +139,13 @@ struct KParams {
     uint32_t* surv;                 // queued candidates: kRefSlots (255) slots per k_eval_ref block
     unsigned* surv_count;           // [k_eval_ref blocks] slots used (zeroed before each k_eval_ref)
     unsigned* surv_pre;             // [k_eval_ref blocks + 1] their exclusive prefix (k_tail_scan)
+    uint32_t* surv_dense;           // the survivors in block order (k_tail_compact)
     float4* psum;                   // [Pc] (patch sum w, sum w r, sum w r^2, centre texel) for the tail
     // k_eval_nb's deferred interpolation fallbacks (ncc_chunk, k_nb_fix): pixel << 8 | hypothesis << 5 |
     // view; null = none (fallbacks inline)
-    uint32_t* nbfix;
-    unsigned* nbfix_count;
-    unsigned nbfix_cap;
+    uint32_t* nbfix;                // kNbFixRegions regions of nbfix_cap entries
+    unsigned* nbfix_count;          // [kNbFixRegions]
+    unsigned nbfix_cap;             // entries per region
 };
 
 // Per-half-sweep output buffers of the colour being updated.

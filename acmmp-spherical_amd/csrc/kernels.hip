@@ -583,6 +583,13 @@ __device__ __forceinline__ float4 patch_sample(const KParams& kp, int px, int py
     return make_float4(d.x, d.y, d.z, w);
 }
 
+// one sample's terms of SPHERE's patch sums (sum w, sum w r, sum w r r), in the sums' order
+__device__ __forceinline__ void patch_fold_sample(float w, float r, Patch& pt) {
+    pt.sbw += w;
+    pt.sref = fmaf(w, r, pt.sref);
+    pt.srr = fmaf(w * r, r, pt.srr);
+}
+
 // SPHERE's hypothesis- and view-independent weight sums of an unstaged patch (the staged layouts
 // form them in coop_patch_nb / coop_patch_sep, in the same order).
 template <int MODEL>
@@ -593,9 +600,7 @@ __device__ __forceinline__ void patch_sums(const KParams& kp, Patch& pt, int px,
             float r;
             const float w = patch_sample<MODEL>(kp, px, py, s, -kp.R + (s / kp.nside) * kp.inc,
                                                 -kp.R + (s % kp.nside) * kp.inc, pt.center, r).w;
-            pt.sbw += w;
-            pt.sref = fmaf(w, r, pt.sref);
-            pt.srr = fmaf(w * r, r, pt.srr);
+            patch_fold_sample(w, r, pt);
         }
     }
 }
@@ -640,8 +645,26 @@ __device__ __forceinline__ float ncc_cost(float sbw, f32x2 srrr, f32x2 ssrs, flo
 
 // One SPHERE view's (sum w s, sum w r s) and sum w s s with every one of the 36 samples projected in the
 // fast arithmetic, in patch order (ACMMP.cu:456-498): the interpolated loop's fallback, inline in
-// ncc_chunk or deferred to k_nb_fix.  sample(s, rw, r): sample s's (ray, w) and reference texel, from the
-// staged patch or recomputed -- the same values either way, so the same bits.
+// ncc_chunk or deferred to k_nb_fix.  sphere_sample_texel: one sample's source texel; sphere_fold_sample:
+// its terms, in the order of the sums (k_nb_fix folds the same values in the same order, so the same bits).
+template <int TEX, typename Cam>
+__device__ __forceinline__ float sphere_sample_texel(Cam& c, float4 ph, __amdgpu_buffer_rsrc_t rs, float4 rw) {
+    const float dep = depth_from_plane_fast(ph, rw);
+    float x, y;
+    project_fast<kSphere>(c, cam_point_fast<kSphere>(c, 0, 0, dep, rw), x, y);
+    x = fmaf(-floorf(x * c.invW), c.Wf, x);
+    y = __builtin_amdgcn_fmed3f(y, 0.0f, c.Hm1f);
+    return lerp_tap<TEX>(fetch_tap<TEX, true>(rs, c, x, y));
+}
+
+__device__ __forceinline__ void sphere_fold_sample(float w, float r, float sp, f32x2& ssrs, float& sss) {
+    const f32x2 wwr = (f32x2){w, w * r};
+    ssrs = pk_fma(wwr, splat2(sp), ssrs);
+    const float ws = w * sp;
+    sss = fmaf(ws, sp, sss);
+}
+
+// sample(s, rw, r): sample s's (ray, w) and reference texel, from the staged patch
 template <int TEX, typename Cam, typename SampleF>
 __device__ __forceinline__ void sphere_view_sums(Cam& c, float4 ph, __amdgpu_buffer_rsrc_t rs, SampleF&& sample,
                                                  f32x2& ssrs, float& sss) {
@@ -652,27 +675,21 @@ __device__ __forceinline__ void sphere_view_sums(Cam& c, float4 ph, __amdgpu_buf
         float4 rw;
         float r;
         sample(s, rw, r);
-        const float dep = depth_from_plane_fast(ph, rw);
-        float x, y;
-        project_fast<kSphere>(c, cam_point_fast<kSphere>(c, 0, 0, dep, rw), x, y);
-        x = fmaf(-floorf(x * c.invW), c.Wf, x);
-        y = __builtin_amdgcn_fmed3f(y, 0.0f, c.Hm1f);
-        const Tap t = fetch_tap<TEX, true>(rs, c, x, y);
-        const float w = rw.w;
-        const f32x2 wwr = (f32x2){w, w * r};
-        const float sp = lerp_tap<TEX>(t);
-        ssrs = pk_fma(wwr, splat2(sp), ssrs);
-        const float ws = w * sp;
-        sss = fmaf(ws, sp, sss);
+        sphere_fold_sample(rw.w, r, sphere_sample_texel<TEX>(c, ph, rs, rw), ssrs, sss);
     }
 }
 
 // fixkey: k_eval_nb's (pixel << 8 | hypothesis << 5) for deferring interpolation fallbacks to k_nb_fix;
-// ~0u: none (every other caller, the fallback runs inline)
+// kFixInline: the fallback runs inline (k_eval_nb / the test hook without a queue); kFixNone (the
+// default): no fallback -- the refinement kernels' interpolated instances (V > 4), whose inline fallbacks
+// cost C3 6.6 ms per half-sweep (random candidates; profiles/r04_prof_ab.txt) and which the float64 study
+// finds within 1e-4 on every pole / seam / random query tried from 2000x1000 up except pole-straddling
+// patches (k_eval_nb, which takes the most hypotheses, keeps the fallback)
+constexpr uint32_t kFixNone = ~0u, kFixInline = ~0u - 1u;
 template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM = 0, bool FULL = false>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv_rt, float (&cost)[VB],
-                                          uint32_t fixkey = ~0u) {
+                                          uint32_t fixkey = kFixNone) {
     // FULL: every view of the chunk present (compile-time); otherwise a wave-uniform count, kept in an
     // SGPR so the per-view guards are scalar branches (without it they were lane masks round-tripped
     // through a VGPR: two VALU per view-sample)
@@ -790,7 +807,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             constexpr float kL1[4] = {0.26666667f, 1.3333334f, -0.6666667f, 0.06666667f};
             constexpr float kL4[4] = {0.06666667f, -0.6666667f, 1.3333334f, 0.26666667f};
             constexpr int kNode[4] = {0, 2, 3, 5};
-            constexpr float kSpreadMax = 64.0f;     // source pixels spanned by the corner nodes (see below)
+            const float spread_max = kp.spread_max;     // source pixels spanned by the corner nodes (see below)
             uint32_t rough = 0u;                        // views whose nodes spread too far (below)
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
@@ -858,7 +875,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                     }
                 }
                 // The interpolation holds where the source mapping is smooth over the patch.  Where the four
-                // corner nodes spread over more than kSpreadMax source pixels in x or y -- a patch landing
+                // corner nodes spread over more than kp.spread_max source pixels in x or y -- a patch landing
                 // next to a source pole (longitude stretches as 1 / cos(latitude)) or a near-grazing plane
                 // whose depth flips sign inside the patch -- the lane projects all 36 samples instead, in the
                 // per-sample loop's order and arithmetic (so those costs are the per-sample fast ones bit for
@@ -869,7 +886,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                                   fminf(fminf(nd[0][3].x, nd[3][0].x), fminf(nd[3][3].x, 0.0f));
                 const float sy_ = fmaxf(fmaxf(nd[0][0].y, nd[0][3].y), fmaxf(nd[3][0].y, nd[3][3].y)) -
                                   fminf(fminf(nd[0][0].y, nd[0][3].y), fminf(nd[3][0].y, nd[3][3].y));
-                const bool smooth = fmaxf(sx_, sy_) <= kSpreadMax;
+                const bool smooth = fmaxf(sx_, sy_) <= spread_max;
                 rough |= smooth ? 0u : (1u << v);
                 // the samples re-read (w, r) from LDS rather than keep the nodes' reads live across the
                 // projections (merged, they spilled 210 VGPRs)
@@ -900,19 +917,22 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             // queue.  After the view loop, with no node live (inside it the queue's code spilled).
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
-                if (!has(v)) continue;
+                if (!has(v) || fixkey == kFixNone) continue;
                 bool redo = (rough >> v) & 1u;
-                if (fixkey != ~0u) {
+                if (fixkey != kFixInline) {
                     const unsigned long long b = __ballot(redo);
                     if (b) {
                         const int lane = __lane_id();
                         const int leader = __ffsll(static_cast<long long>(b)) - 1;
                         unsigned base = 0u;
-                        if (lane == leader) base = atomicAdd(kp.nbfix_count, static_cast<unsigned>(__popcll(b)));
+                        // one of kNbFixRegions counters per block (a single one serialised the atomics: k_eval_nb
+                        // +0.35 ms at the metric)
+                        const unsigned region = blockIdx.x % kNbFixRegions;
+                        if (lane == leader) base = atomicAdd(kp.nbfix_count + region, static_cast<unsigned>(__popcll(b)));
                         base = __shfl(base, leader);
                         const unsigned slot = base + static_cast<unsigned>(__popcll(b & ((1ull << lane) - 1ull)));
                         if (redo && slot < kp.nbfix_cap) {
-                            kp.nbfix[slot] = fixkey | static_cast<uint32_t>(cv[v] - 1);
+                            kp.nbfix[static_cast<long long>(region) * kp.nbfix_cap + slot] = fixkey | static_cast<uint32_t>(cv[v] - 1);
                             redo = false;
                         }
                     }
@@ -1217,7 +1237,7 @@ __device__ __forceinline__ float4 perturbed_normal(float4 v, float4 n, Rng& rs, 
 // Evaluate all source views of plane `ph` and hand each cost to f(view0, cost) in view order.
 template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM, typename F>
 __device__ __forceinline__ void for_all_views_t(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
-                                                uint32_t wave_mask, F&& f, uint32_t fixkey = ~0u) {
+                                                uint32_t wave_mask, F&& f, uint32_t fixkey = kFixNone) {
     int v = 0;
     const int V = kp.V;
     while (true) {
@@ -1732,10 +1752,7 @@ __device__ __forceinline__ Patch coop_patch_nb(const KParams& kp, bool valid, in
     pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f;
     if (MODEL == kSphere && valid) {
         for (int s = 0; s < kp.S; ++s) {                // patch_sums order (ACMMP.cu:482-486)
-            const float w = rw[s * NPIX].z, r = rw[s * NPIX].w;
-            pt.sbw += w;
-            pt.sref = fmaf(w, r, pt.sref);
-            pt.srr = fmaf(w * r, r, pt.srr);
+            patch_fold_sample(rw[s * NPIX].z, rw[s * NPIX].w, pt);
         }
     }
     return pt;
@@ -1775,10 +1792,7 @@ __device__ __forceinline__ Patch coop_patch_sep(const KParams& kp, bool valid, i
     pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f;
     if (valid) {
         for (int s = 0; s < kp.S; ++s) {                // patch_sums order (ACMMP.cu:482-486)
-            const float w = wr[s].x, r = wr[s].y;
-            pt.sbw += w;
-            pt.sref = fmaf(w, r, pt.sref);
-            pt.srr = fmaf(w * r, r, pt.srr);
+            patch_fold_sample(wr[s].x, wr[s].y, pt);
         }
     }
     return pt;
@@ -1793,6 +1807,17 @@ __device__ __forceinline__ Patch coop_patch_sep(const KParams& kp, bool valid, i
 constexpr bool kRefPipe = true;
 template <int MODEL, int VB>
 constexpr int ref_vb() { return (VB == 4 || (VB > 4 && MODEL == kSphere)) ? 2 : (VB > kEvalVB ? kEvalVB : VB); }
+#ifndef ACMMP_REF_PIN_VB
+#define ACMMP_REF_PIN_VB 4
+#endif
+// k_eval_ref's chunk: the fast pinhole chunks' homogeneous points hold ~12 VGPRs per view across the sample loop
+template <int MODEL, int VB, int TF>
+constexpr int ref_vb_eval() {
+    return (MODEL == kPinhole && TF == 2 && ref_vb<MODEL, VB>() > ACMMP_REF_PIN_VB) ? ACMMP_REF_PIN_VB : ref_vb<MODEL, VB>();
+}
+#ifndef ACMMP_REF_WAVES
+#define ACMMP_REF_WAVES 1
+#endif
 constexpr int kRefLanes = 5;                // refinement candidates (ACMMP.cu:870)
 constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 lanes used)
 constexpr int kRefSlots = kRefPix * kRefLanes;  // survivor slots per k_eval_ref block
@@ -1841,40 +1866,82 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? 7 : 8) : 1) void k_ev
     const float4 ph = plane_at(kp, pos);
     const uint32_t all = kp.nb_views;
     float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
-    const uint32_t fixkey = kp.nbfix ? (static_cast<uint32_t>(ci) << 8) | (static_cast<uint32_t>(h) << 5) : ~0u;
+    const uint32_t fixkey = kp.nbfix ? (static_cast<uint32_t>(ci) << 8) | (static_cast<uint32_t>(h) << 5) : kFixInline;
     for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
         kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; }, fixkey);
 }
 
 // The interpolation fallbacks k_eval_nb queued (ncc_chunk): each (pixel, hypothesis, view) cost with every
-// sample projected, the patch recomputed (make_patch: the staged values and sums, the same bits), over
-// the same hyp_cost entry k_eval_nb wrote.  One lane per entry, after every k_eval_nb launch of the
-// half-sweep and before k_select.
+// sample projected, the patch recomputed (its samples, weights and sums: the same bits as the staged
+// ones), over the same hyp_cost entry k_eval_nb wrote; after every k_eval_nb launch of the half-sweep and
+// before k_select.  kFixLanes lanes per entry: lane j takes patch row j's samples (reference texel, weight,
+// ray, source texel) into LDS, then lane 0 folds the 36 in patch order with patch_fold_sample /
+// sphere_fold_sample -- the inline fallback's values in its order, so its bits.  One lane per entry, each
+// running 72 dependent sample chains (the patch sums, then the view sums), took 0.10 ms per launch at
+// the metric, latency-bound (profiles/r04_ab3_kernel_stats.csv).
+constexpr int kFixLanes = 6, kFixPerWave = 64 / kFixLanes, kFixPerBlock = 4 * kFixPerWave;
+
+// Lane j (< kFixLanes) of a fallback entry: patch row j's samples into smp[s] = (w, r, source texel)
+template <int TEX>
+__device__ __forceinline__ void fix_row(const KParams& kp, int px, int py, float4 ph, int v, int j, float4* smp) {
+    typedef const __attribute__((address_space(4))) DevCam ConstCam;
+    const DevCam& rc = kp.cams[0];
+    const float center = texel_padded(rc.img_base, rc.img_pitch, rc.W, rc.H, px, py);
+    ConstCam& c = ((ConstCam*)(kp.cams))[v + 1];
+    const __amdgpu_buffer_rsrc_t rs = TEX == 1
+        ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000)
+        : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(c.img_base), 0, c.img_bytes, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int s = j * 6 + k;
+        float r;
+        const float4 rw = patch_sample<kSphere>(kp, px, py, s, -kp.R + j * kp.inc, -kp.R + k * kp.inc, center, r);
+        smp[s] = make_float4(rw.w, r, sphere_sample_texel<TEX>(c, ph, rs, rw), 0.f);
+    }
+}
+
+// Lane 0 of a fallback entry: the NCC from the 36 staged samples
+__device__ __forceinline__ float fix_fold(const float4* smp) {
+    Patch pt;
+    pt.sbw = 0.f; pt.sref = 0.f; pt.srr = 0.f;
+    f32x2 ssrs = splat2(0.f);
+    float sss = 0.f;
+#pragma unroll 6
+    for (int s = 0; s < 36; ++s) {
+        const float4 q = smp[s];
+        patch_fold_sample(q.x, q.y, pt);
+        sphere_fold_sample(q.x, q.y, q.z, ssrs, sss);
+    }
+    return ncc_cost(pt.sbw, (f32x2){pt.sref, pt.srr}, ssrs, sss);
+}
+
+// block b of the fix grid takes region b % kNbFixRegions, its (b / kNbFixRegions)-th stripe of entries
 template <int TEX>
 __global__ __launch_bounds__(256) void k_nb_fix(const KParams kp, const int colour) {
-    const unsigned n = min(*kp.nbfix_count, kp.nbfix_cap);
+    __shared__ float4 smp[kFixPerBlock][36];
+    const int t = threadIdx.x, l = t & 63;
+    const int ew = l / kFixLanes, j = l - ew * kFixLanes, e = (t >> 6) * kFixPerWave + ew;
+    const unsigned region = blockIdx.x % kNbFixRegions, stripes = gridDim.x / kNbFixRegions;
+    const unsigned n = min(kp.nbfix_count[region], kp.nbfix_cap);
+    const uint32_t* q = kp.nbfix + static_cast<long long>(region) * kp.nbfix_cap;
     const long long Pc = kp.Pc;
-    typedef const __attribute__((address_space(4))) DevCam ConstCam;
-    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        const uint32_t key = kp.nbfix[i];
-        const long long ci = key >> 8;
-        const int h = static_cast<int>((key >> 5) & 7u), v = static_cast<int>(key & 31u);
-        const int py = static_cast<int>(ci / kp.Wh);
-        const int px = 2 * static_cast<int>(ci - static_cast<long long>(py) * kp.Wh) + ((py + colour) & 1);
-        const float4 ph = plane_at(kp, kp.nbpos[h * Pc + ci]);
-        const Patch pt = make_patch<kSphere>(kp, px, py);
-        ConstCam& c = ((ConstCam*)(kp.cams))[v + 1];
-        const __amdgpu_buffer_rsrc_t rs = TEX == 1
-            ? __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000)
-            : __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(c.img_base), 0, c.img_bytes, 0x00020000);
-        f32x2 ssrs;
-        float sss;
-        sphere_view_sums<TEX>(c, ph, rs, [&](int s, float4& rw, float& r) {
-            const int ii = s / kp.nside, jj = s - ii * kp.nside;
-            rw = patch_sample<kSphere>(kp, px, py, s, -kp.R + ii * kp.inc, -kp.R + jj * kp.inc, pt.center, r);
-        }, ssrs, sss);
-        kp.hyp_cost[(static_cast<long long>(h) * kp.V + v) * Pc + ci] =
-            ncc_cost(pt.sbw, (f32x2){pt.sref, pt.srr}, ssrs, sss);
+    for (unsigned i0 = (blockIdx.x / kNbFixRegions) * kFixPerBlock; i0 < n; i0 += stripes * kFixPerBlock) {
+        const unsigned i = i0 + static_cast<unsigned>(e);
+        const bool act = ew < kFixPerWave && i < n;
+        long long ci = 0;
+        int h = 0, v = 0;
+        if (act) {
+            const uint32_t key = q[i];
+            ci = key >> 8;
+            h = static_cast<int>((key >> 5) & 7u);
+            v = static_cast<int>(key & 31u);
+            const int py = static_cast<int>(ci / kp.Wh);
+            const int px = 2 * static_cast<int>(ci - static_cast<long long>(py) * kp.Wh) + ((py + colour) & 1);
+            fix_row<TEX>(kp, px, py, plane_at(kp, kp.nbpos[h * Pc + ci]), v, j, smp[e]);
+        }
+        __syncthreads();
+        if (act && j == 0) kp.hyp_cost[(static_cast<long long>(h) * kp.V + v) * Pc + ci] = fix_fold(smp[e]);
+        __syncthreads();
     }
 }
 
@@ -2214,7 +2281,7 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
 
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
 template <int MODEL, int VB, bool GEOM, int TF>
-__global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int colour) {
+__global__ __launch_bounds__(256, ACMMP_REF_WAVES) void k_eval_ref(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
@@ -2235,7 +2302,7 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
     Patch pt;
     if constexpr (kStaged == 4) pt = coop_patch_sep<kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
     else pt = coop_patch_nb<MODEL, kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
-    constexpr int VBA = ref_vb<MODEL, VB>();
+    constexpr int VBA = ref_vb_eval<MODEL, VB, TF>();
     if (!valid) return;
     if (kp.ref_split > 0 && h == 0) {                        // the tail's patch, without re-summing it
         const DevCam& rc = kp.cams[0];
@@ -2317,6 +2384,13 @@ __global__ __launch_bounds__(1024) void k_tail_scan(const KParams kp, const int 
     }
     if (t == 1023) kp.surv_pre[nref] = part[1023];
 }
+
+// The survivors in k_eval_ref block order, dense: block b's slots to surv_dense[surv_pre[b] ...].
+__global__ __launch_bounds__(256) void k_tail_compact(const KParams kp) {
+    const int b = blockIdx.x, r = threadIdx.x;
+    if (r < static_cast<int>(kp.surv_count[b]))
+        kp.surv_dense[kp.surv_pre[b] + r] = kp.surv[static_cast<long long>(b) * kRefSlots + r];
+}
 #endif  // ACMMP_IN_TU(4)
 
 // The queued candidates' views [ref_split, V) (one lane per candidate, patch samples recomputed),
@@ -2325,32 +2399,18 @@ __global__ __launch_bounds__(1024) void k_tail_scan(const KParams kp, const int 
 // segments (blocks b and b + 8 share an XCD's L2): each XCD's resident blocks walk a window of a few
 // rows, so the source footprints its L2 holds are those rows' (a queue shared by all blocks, filled in
 // wave completion order, gave C3 a 58% L2 hit rate and 36 GB per launch), and every lane has a survivor
-// (per-k_eval_ref-block tail blocks left half their lanes idle).
+// (per-k_eval_ref-block tail blocks left half their lanes idle; a binary search of surv_pre per 256 survivors
+// serialised each block: the metric's tail 0.34 -> 1.2 ms).
 template <int MODEL, int VB, bool GEOM, int TF>
 __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const int colour, const int nref) {
-    __shared__ int first_block;
     const unsigned total = kp.surv_pre[nref];
     const unsigned x = blockIdx.x & 7u, k = blockIdx.x >> 3, nk = gridDim.x >> 3;
     const unsigned seg0 = static_cast<unsigned>(static_cast<unsigned long long>(total) * x / 8u);
     const unsigned seg1 = static_cast<unsigned>(static_cast<unsigned long long>(total) * (x + 1u) / 8u);
     const long long Pc = kp.Pc;
     const int S = kp.ref_split;
-    for (unsigned c0 = seg0 + k * 256u; c0 < seg1; c0 += nk * 256u) {
-        if (threadIdx.x == 0) {                              // the k_eval_ref block holding survivor c0
-            int lo = 0, hi = nref - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (kp.surv_pre[mid] <= c0) lo = mid; else hi = mid - 1;
-            }
-            first_block = lo;
-        }
-        __syncthreads();
-        int b = first_block;
-        __syncthreads();
-        const unsigned i = c0 + threadIdx.x;
-        if (i >= seg1) continue;
-        while (kp.surv_pre[b + 1] <= i) ++b;
-        const uint32_t rec = kp.surv[static_cast<long long>(b) * kRefSlots + (i - kp.surv_pre[b])];
+    for (unsigned i = seg0 + k * 256u + threadIdx.x; i < seg1; i += nk * 256u) {
+        const uint32_t rec = kp.surv_dense[i];
         const long long ci = rec >> 3;
         const int h = static_cast<int>(rec & 7u);
         const int py = static_cast<int>(ci / kp.Wh);
@@ -2724,7 +2784,7 @@ hipError_t launch_eval_nb(const KParams& kp0, int colour, hipStream_t s) {
     const bool fix = kp.nbfix && kp.model == kSphere && kp.fast && kp.tex16 && kp.interp;
     if (!fix) kp.nbfix = nullptr;
     hipError_t e0 = hipSuccess;
-    if (fix && (e0 = hipMemsetAsync(kp.nbfix_count, 0, sizeof(unsigned), s)) != hipSuccess) return e0;
+    if (fix && (e0 = hipMemsetAsync(kp.nbfix_count, 0, sizeof(unsigned) * kNbFixRegions, s)) != hipSuccess) return e0;
     const int chunk = nb_view_chunk(kp);
     for (int v0 = 0; v0 < kp.V; v0 += chunk) {
         const int v1 = std::min(kp.V, v0 + chunk);
@@ -2735,7 +2795,7 @@ hipError_t launch_eval_nb(const KParams& kp0, int colour, hipStream_t s) {
         if (e != hipSuccess) return e;
     }
     if (fix) {
-        k_nb_fix<1><<<1024, 256, 0, s>>>(kp, colour);
+        k_nb_fix<1><<<16 * kNbFixRegions, 256, 0, s>>>(kp, colour);   // 16 stripes per region
         return hipGetLastError();
     }
     return hipSuccess;
@@ -2762,12 +2822,48 @@ __global__ __launch_bounds__(256) void k_debug_nb(const KParams kp, int n, const
     const float4 ph = planes[k];
     float* o = out + k * kp.V;
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
+    const uint32_t fixkey = kp.nbfix ? (static_cast<uint32_t>(q) << 8) | (static_cast<uint32_t>(h) << 5) : kFixInline;
     for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
-        kp, px, py, pt, ph, all, [&](int v, float c) { o[v] = c; });
+        kp, px, py, pt, ph, all, [&](int v, float c) { o[v] = c; }, fixkey);
 }
 
-hipError_t launch_debug_nb(const KParams& kp, int n, const int* px, const int* py, const float4* planes, float* out,
+// The hook's deferred fallbacks (k_nb_fix for query pixels and planes)
+template <int TEX>
+__global__ __launch_bounds__(256) void k_debug_nb_fix(const KParams kp, const int* __restrict__ qx,
+                                                      const int* __restrict__ qy, const float4* __restrict__ planes,
+                                                      float* __restrict__ out) {
+    __shared__ float4 smp[kFixPerBlock][36];
+    const int t = threadIdx.x, l = t & 63;
+    const int ew = l / kFixLanes, j = l - ew * kFixLanes, e = (t >> 6) * kFixPerWave + ew;
+    const unsigned region = blockIdx.x % kNbFixRegions, stripes = gridDim.x / kNbFixRegions;
+    const unsigned n = min(kp.nbfix_count[region], kp.nbfix_cap);
+    const uint32_t* qu = kp.nbfix + static_cast<long long>(region) * kp.nbfix_cap;
+    for (unsigned i0 = (blockIdx.x / kNbFixRegions) * kFixPerBlock; i0 < n; i0 += stripes * kFixPerBlock) {
+        const unsigned i = i0 + static_cast<unsigned>(e);
+        const bool act = ew < kFixPerWave && i < n;
+        long long k = 0;
+        int v = 0;
+        if (act) {
+            const uint32_t key = qu[i];
+            const int qq = static_cast<int>(key >> 8), h = static_cast<int>((key >> 5) & 7u);
+            v = static_cast<int>(key & 31u);
+            k = static_cast<long long>(qq) * kNbLanes + h;
+            fix_row<TEX>(kp, qx[qq], qy[qq], planes[k], v, j, smp[e]);
+        }
+        __syncthreads();
+        if (act && j == 0) out[k * kp.V + v] = fix_fold(smp[e]);
+        __syncthreads();
+    }
+}
+
+hipError_t launch_debug_nb(const KParams& kp0, int n, const int* px, const int* py, const float4* planes, float* out,
                            hipStream_t s) {
+    // the hook takes k_eval_nb's path, deferred fallbacks included (ACMMP_NB_FIX=0: inline)
+    KParams kp = kp0;
+    const bool fix = kp.nbfix && kp.model == kSphere && kp.fast && kp.tex16 && kp.interp && n < (1 << 24);
+    if (!fix) kp.nbfix = nullptr;
+    hipError_t e0 = hipSuccess;
+    if (fix && (e0 = hipMemsetAsync(kp.nbfix_count, 0, sizeof(unsigned) * kNbFixRegions, s)) != hipSuccess) return e0;
     const size_t lds_nb = nb_lds_bytes(kp.model, kp.S, kp.nside);
     const dim3 grd = static_cast<unsigned>(cdiv(n, kNbPix));
     if (kp.fast) {
@@ -2777,6 +2873,7 @@ hipError_t launch_debug_nb(const KParams& kp, int n, const int* px, const int* p
         if (kp.tex16) ACMMP_DISPATCH(kp.model, kp.V, (k_debug_nb<M, VBC, 1, 0><<<grd, 256, lds_nb, s>>>(kp, n, px, py, planes, out)));
         else ACMMP_DISPATCH(kp.model, kp.V, (k_debug_nb<M, VBC, 0, 0><<<grd, 256, lds_nb, s>>>(kp, n, px, py, planes, out)));
     }
+    if (fix) k_debug_nb_fix<1><<<kNbFixRegions, 256, 0, s>>>(kp, px, py, planes, out);
     return hipGetLastError();
 }
 
@@ -2819,6 +2916,7 @@ hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s) {
         // known on the device only: nk covers the largest possible queue, up to 256 blocks per XCD)
         const int nref = static_cast<int>(grd_ref.x);
         k_tail_scan<<<1, 1024, 0, s>>>(kp, nref);
+        k_tail_compact<<<static_cast<unsigned>(nref), 256, 0, s>>>(kp);
         const unsigned grd = 8u * static_cast<unsigned>(std::min<long long>(256, std::max<long long>(1, cdiv(static_cast<long long>(nref) * kRefSlots, 8 * 256))));
         if (kp.geom) ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, true, TF><<<grd, 256, 0, s>>>(kp, colour, nref))));
         else ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, false, TF><<<grd, 256, 0, s>>>(kp, colour, nref))));

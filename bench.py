@@ -85,7 +85,7 @@ def eval_nb_executed_flop_per_pixel_pinhole(V: int, samples: int = 36) -> float:
 def interp_enabled(width: int, height: int, patch_size: int = 11, radius_increment: int = 2) -> bool:
     """capi.cpp build_kparams' gate (tests/np_interp.interp_enabled)."""
     R = patch_size // 2
-    return len(range(-R, R + 1, radius_increment)) == 6 and 1600 * R <= 5 * width and 800 * R <= 5 * height
+    return len(range(-R, R + 1, radius_increment)) == 6 and 2000 * R <= 5 * width and 1000 * R <= 5 * height
 
 
 def parse():

@@ -88,7 +88,7 @@ def ncc(images, cams, params, src, px, py, plane, interp, order=3, span_max=None
 
 
 NODES = [-5, -1, 1, 5]          # patch offsets of node columns / rows {0, 2, 3, 5} at patch_size 11, increment 2
-SPREAD_MAX = 64.0               # kernels.hip kSpreadMax: beyond it the lane projects every sample of the view
+SPREAD_MAX = 256.0              # kernels.hip kSpreadMax: beyond it the lane projects every sample of the view
 
 
 def nodes_for(params):
@@ -100,9 +100,9 @@ def nodes_for(params):
 
 
 def interp_enabled(W, H, params):
-    """capi.cpp build_kparams' gate: 6x6 SPHERE patches whose radius spans at most 5 pixels of 2 pi / 1600."""
+    """capi.cpp build_kparams' gate: 6x6 SPHERE patches whose radius spans at most 5 pixels of 2 pi / 2000."""
     R, inc = int(params["patch_size"]) // 2, int(params["radius_increment"])
-    return len(range(-R, R + 1, inc)) == 6 and 1600 * R <= 5 * W and 800 * R <= 5 * H
+    return len(range(-R, R + 1, inc)) == 6 and 2000 * R <= 5 * W and 1000 * R <= 5 * H
 
 
 def surface_projections(sc, stride=2, margin=6):

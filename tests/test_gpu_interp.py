@@ -203,3 +203,43 @@ def test_pinhole_homogeneous_k_eval_nb_per_query(ctx, name, monkeypatch):
         os.makedirs(out_dir, exist_ok=True)
         with open(os.path.join(out_dir, f"pinhole_queries_{name}.json"), "w") as fh:
             json.dump(report, fh, indent=1)
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_deferred_fallbacks_per_query_bit_identical(ctx, name, monkeypatch):
+    """acmmp_debug_ncc_nb runs k_eval_nb's path including the deferred interpolation fallbacks (queued in
+    ncc_chunk, recomputed by k_debug_nb_fix like k_nb_fix); inline (ACMMP_NB_FIX=0) the lane recomputes them
+    itself.  The same costs bit for bit on the pole / seam / random query sets."""
+    make, _ = CONFIGS[name]
+    sc = make()
+    c0 = sc.cameras[0]
+    p = types.default_params(num_images=len(sc.images), depth_min=float(c0["depth_min"]) * 0.6,
+                             depth_max=float(c0["depth_max"]) * 1.2)
+    ctx.set_params(p)
+    ctx.upload_views(sc.images, sc.cameras)
+    ctx.set_math("fast")
+    for kind, n in KINDS.items():
+        px, py, _ = ni.special_pixels(sc, kind, n, seed=len(kind) + 17)
+        planes = ni.near_surface_planes(sc, px, py, 8, seed=len(kind) + 29)
+        planes[:, 4:] = ni.near_surface_planes(sc, px, py, 4, seed=len(kind) + 31, spread=1.5, depth_jitter=0.4)
+        for spread in ("256", "4"):   # the product threshold; a small one so that most lanes fall back
+            monkeypatch.setenv("ACMMP_SPREAD_MAX", spread)
+            ctx.set_params(p)
+            queued = ctx.debug_ncc_nb(px, py, planes)
+            monkeypatch.setenv("ACMMP_NB_FIX", "0")
+            ctx.set_params(p)
+            inline = ctx.debug_ncc_nb(px, py, planes)
+            monkeypatch.delenv("ACMMP_NB_FIX")
+            bad = np.nonzero(queued.view(np.uint32) != inline.view(np.uint32))
+            assert bad[0].size == 0, (kind, spread, bad[0].size,
+                                      [(int(a), int(b), int(c), float(queued[a, b, c]), float(inline[a, b, c]))
+                                       for a, b, c in zip(*bad)][:5])
+        # the small threshold did send lanes to the fallback: their costs are the per-sample ones, not the
+        # interpolated ones
+        monkeypatch.setenv("ACMMP_SPREAD_MAX", "1e30")
+        ctx.set_params(p)
+        interp_only = ctx.debug_ncc_nb(px, py, planes)
+        monkeypatch.delenv("ACMMP_SPREAD_MAX")
+        ctx.set_params(p)
+        assert np.mean(interp_only.view(np.uint32) != queued.view(np.uint32)) > 0.2, kind
+    ctx.set_math("exact")

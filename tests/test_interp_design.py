@@ -2,9 +2,10 @@
 projecting a 6x6 patch exactly at the samples of columns / rows {0, 2, 3, 5} and taking the 4-point
 Lagrange interpolation for the others changes the float64 NCC (tests/np_reference.py's restatement of
 ComputeBilateralNCC, ACMMP.cu:405-516) by less than the binary32 noise floor (1e-4) for near-surface and
-random planes once a reference pixel spans at most 2 pi / 1600 rad, except on the rare hypotheses whose
-16 nodes spread far in the source (grazing planes, patches landing next to a source pole) -- those the
-kernel projects in full (capi.cpp build_kparams' gate; kernels.hip ncc_chunk's spread test).
+random planes once a reference pixel spans at most 2 pi / 2000 rad, except on the rare hypotheses whose
+corner nodes spread over more than 256 source pixels (patches on a source pole) -- those the kernel projects
+in full (capi.cpp build_kparams' gate; kernels.hip ncc_chunk's spread test).  At 1600x800 a 256-pixel test
+misses a pole case (3.7e-3 at a 65-pixel spread): the gate starts at 2000x1000.
 CPU, float64; the kernel itself is queried per hypothesis in tests/test_gpu_interp.py.
 """
 import numpy as np
@@ -32,12 +33,12 @@ def _queries(sc, p, rng, n, W, H, margin=6):
 
 
 def test_interpolated_ncc_within_noise_floor():
-    W, H = 1600, 800
+    W, H = 2000, 1000
     sc = scene.sphere_scene(W, H, n_src=3, seed=2)
     c0 = sc.cameras[0]
     p = types.default_params(num_images=len(sc.images), depth_min=float(c0["depth_min"]) * 0.6,
                              depth_max=float(c0["depth_max"]) * 1.2)
-    assert ni.interp_enabled(W, H, p) and not ni.interp_enabled(1280, 640, p)
+    assert ni.interp_enabled(W, H, p) and not ni.interp_enabled(1600, 800, p)
     worst, n = 0.0, 0
     for px, py, plane in _queries(sc, p, np.random.default_rng(3), 40, W, H):
         for v in range(1, len(sc.images)):
@@ -54,19 +55,19 @@ def test_interpolated_ncc_within_noise_floor():
 
 def test_interpolation_gate_other_patch_geometries():
     """Every (patch_size, radius_increment) the gate admits with 6x6 samples is the validated angular span
-    or finer: patch 21 / increment 4 (also 6x6) spans twice the angle and only interpolates from 3200x1600,
-    where its radius covers the same angle as patch 11 at 1600x800; the 4-point weights are in index space,
-    so its nodes are offsets {-10, -2, 2, 10}.  At 3200x1600 the study covers it in float64."""
+    or finer: patch 21 / increment 4 (also 6x6) spans twice the angle and only interpolates from 4000x2000,
+    where its radius covers the same angle as patch 11 at 2000x1000; the 4-point weights are in index space,
+    so its nodes are offsets {-10, -2, 2, 10}."""
     for ps, inc in ((11, 2), (21, 4), (13, 2), (9, 2), (11, 1)):
         p = types.default_params(patch_size=ps, radius_increment=inc)
         R = ps // 2
         six = len(range(-R, R + 1, inc)) == 6
-        for W, H in ((1280, 640), (1600, 800), (2000, 1500), (3200, 1600), (4096, 2048)):
+        for W, H in ((1280, 640), (1600, 800), (2000, 1000), (2000, 1500), (3200, 1600), (4096, 2048)):
             on = ni.interp_enabled(W, H, p)
-            assert on == (six and 2 * np.pi * R / W <= 2 * np.pi * 5 / 1600 + 1e-12 and np.pi * R / H <= np.pi * 5 / 800 + 1e-12)
+            assert on == (six and 2 * np.pi * R / W <= 2 * np.pi * 5 / 2000 + 1e-12 and np.pi * R / H <= np.pi * 5 / 1000 + 1e-12)
     p = types.default_params(patch_size=21, radius_increment=4)
     assert ni.nodes_for(p) == [-10, -2, 2, 10]
-    assert not ni.interp_enabled(2000, 1500, p) and ni.interp_enabled(3200, 1600, p)
+    assert not ni.interp_enabled(3200, 1600, p) and ni.interp_enabled(4096, 2048, p)
 
 
 def test_interpolated_ncc_near_source_poles_and_seam():
@@ -74,7 +75,7 @@ def test_interpolated_ncc_near_source_poles_and_seam():
     landing within 10 degrees of a source pole and across a source's longitude seam, near-surface planes and
     random ones.  With the kernel's spread test every interpolated NCC stays within 1e-4 of the projected one;
     the test is what keeps the pole-adjacent tail there (it falls back on those lanes)."""
-    W, H = 1600, 800
+    W, H = 2000, 1000
     sc = scene.sphere_scene(W, H, n_src=3, seed=5)
     c0 = sc.cameras[0]
     p = types.default_params(num_images=len(sc.images), depth_min=float(c0["depth_min"]) * 0.6,
