@@ -964,6 +964,15 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.color_den = 2.0f * p.sigma_color * p.sigma_color;
     HIP_TRY(c, dreserve(c->d_spatial, c->spatial_cap, static_cast<size_t>(c->model == kSphere ? c->H : 1) * kp.S));
     HIP_TRY(c, launch_spatial_table(kp, c->d_spatial, c->stream));
+    // queue of k_eval_nb's deferred interpolation fallbacks (pixel << 8 | hypothesis << 5 | view: colour
+    // grids below 2^24 pixels), fast SPHERE with interpolated coordinates only: per region (blocks b with
+    // b % kNbFixRegions equal) room for every entry its blocks can queue, kNbPix x 8 hypotheses x the
+    // launch's views each -- so none is ever dropped (metric 193 MB, C3 656 MB)
+    kp.nb_chunk = nb_view_chunk(kp);
+    const bool fixq = c->model == kSphere && c->math == ACMMP_MATH_FAST && c->tex16 && kp.interp &&
+                      Pc < (static_cast<size_t>(1) << 24) && kp.spread_max < 1e30f;
+    const size_t nb_blocks = (static_cast<size_t>(Pc) + kNbPix - 1) / kNbPix;
+    const size_t fix_cap = fixq ? (nb_blocks + kNbFixRegions - 1) / kNbFixRegions * kNbPix * 8 * static_cast<size_t>(kp.nb_chunk) : 0;
     // half-sweep scratch slab: carve the pieces of engine.h's KParams out of one allocation
     size_t off[17];
     {
@@ -973,7 +982,7 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
                                   sizeof(PixState) * Pc, sizeof(float) * VP, sizeof(float) * VP,
                                   sizeof(float) * 5 * VP, sizeof(uint32_t) * (5 * Pc + 256),
                                   sizeof(unsigned) * (Pc / 51 + 2),
-                                  sizeof(float4) * Pc, sizeof(uint32_t) * kNbFixPerPixel * Pc + 1024,
+                                  sizeof(float4) * Pc, sizeof(uint32_t) * kNbFixRegions * fix_cap,
                                   sizeof(unsigned) * kNbFixRegions,
                                   sizeof(unsigned) * (Pc / 51 + 3), sizeof(uint32_t) * (5 * Pc + 256)};
         off[0] = 0;
@@ -1011,15 +1020,11 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.surv = reinterpret_cast<uint32_t*>(c->d_scratch + off[9]);
     kp.surv_count = reinterpret_cast<unsigned*>(c->d_scratch + off[10]);
     kp.psum = reinterpret_cast<float4*>(c->d_scratch + off[11]);
-    // queue of k_eval_nb's deferred interpolation fallbacks (pixel << 8 | hypothesis << 5 | view: colour
-    // grids below 2^24 pixels); a full queue sends the rest back to the inline fallback
-    const char* e_fix = std::getenv("ACMMP_NB_FIX");          // ACMMP_NB_FIX=0: inline fallbacks (A/B)
-    const bool fixq = Pc < (static_cast<size_t>(1) << 24) && !(e_fix && std::atoi(e_fix) == 0);
     kp.nbfix = fixq ? reinterpret_cast<uint32_t*>(c->d_scratch + off[12]) : nullptr;
     kp.nbfix_count = reinterpret_cast<unsigned*>(c->d_scratch + off[13]);
     kp.surv_pre = reinterpret_cast<unsigned*>(c->d_scratch + off[14]);
     kp.surv_dense = reinterpret_cast<uint32_t*>(c->d_scratch + off[15]);
-    kp.nbfix_cap = fixq ? static_cast<unsigned>(kNbFixPerPixel * Pc / kNbFixRegions) : 0u;
+    kp.nbfix_cap = static_cast<unsigned>(fix_cap);
     kp.ref_split = ref_split_point(kp.V, Pc);
     if (!c->d_work) HIP_TRY(c, dalloc(c->d_work, 256));
     kp.work = c->d_work;

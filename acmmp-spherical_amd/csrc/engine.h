@@ -26,7 +26,7 @@ namespace acmmp {
 constexpr int kPinhole = 0;
 constexpr int kSphere = 11;
 constexpr int kMaxViews = 32;       // cost_vector[32], uint32 view bitmask (ACMMP.cu:522,1153)
-constexpr int kNbFixPerPixel = 8;   // queue entries per colour-grid pixel for k_eval_nb's deferred fallbacks
+constexpr int kNbPix = 32;          // k_eval_nb: pixels per 256-lane block (8 lanes each)
 constexpr int kNbFixRegions = 256;  // the queue's regions, one counter each (block % regions)
 
 struct DevCam {
@@ -130,6 +130,7 @@ struct KParams {
     PixState* pst;                  // [Pc]
     unsigned long long* work;       // [256] k_eval_nb pixels with NCC work (SPHERE patch sum >= 1e-6), per block % 256
     uint32_t nb_views;              // k_eval_nb: the source views this launch evaluates (all, or a chunk of them)
+    int nb_chunk;                   // views per k_eval_nb launch (nb_view_chunk)
     int nb_count_work;              // k_eval_nb: this launch adds to `work` (the first launch of a half-sweep)
     long long Pc;                   // H * Wh
     // split refinement: k_eval_ref evaluates views [0, ref_split) of every candidate,
@@ -142,8 +143,8 @@ struct KParams {
     uint32_t* surv_dense;           // the survivors in block order (k_tail_compact)
     float4* psum;                   // [Pc] (patch sum w, sum w r, sum w r^2, centre texel) for the tail
     // k_eval_nb's deferred interpolation fallbacks (ncc_chunk, k_nb_fix): pixel << 8 | hypothesis << 5 |
-    // view; null = none (fallbacks inline)
-    uint32_t* nbfix;                // kNbFixRegions regions of nbfix_cap entries
+    // view; null = none (no interpolation, or ACMMP_SPREAD_MAX off)
+    uint32_t* nbfix;                // kNbFixRegions regions of nbfix_cap entries (every entry a launch can queue)
     unsigned* nbfix_count;          // [kNbFixRegions]
     unsigned nbfix_cap;             // entries per region
 };
@@ -198,6 +199,8 @@ hipError_t launch_export_depth(const float4* planes, long long P, float* dst, hi
 hipError_t launch_copy(const void* src, void* dst, size_t bytes, hipStream_t s);  // bytes % 4 == 0
 hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int sw, int sh, int imagescale,
                       float* out, hipStream_t s);
+// k_eval_nb's source views per launch (kernels.hip, r02 view chunking)
+int nb_view_chunk(const KParams& kp);
 hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,
                         float* out, hipStream_t s);
 // k_eval_nb's NCC instance on n pixels x 8 planes (planes[q * 8 + h]): out[(q * 8 + h) * V + v]

@@ -643,10 +643,9 @@ __device__ __forceinline__ float ncc_cost(float sbw, f32x2 srrr, f32x2 ssrs, flo
     return out;
 }
 
-// One SPHERE view's (sum w s, sum w r s) and sum w s s with every one of the 36 samples projected in the
-// fast arithmetic, in patch order (ACMMP.cu:456-498): the interpolated loop's fallback, inline in
-// ncc_chunk or deferred to k_nb_fix.  sphere_sample_texel: one sample's source texel; sphere_fold_sample:
-// its terms, in the order of the sums (k_nb_fix folds the same values in the same order, so the same bits).
+// The interpolated loop's fallback (k_nb_fix): a SPHERE view's sums with every one of the 36 samples
+// projected in the fast arithmetic, in patch order (ACMMP.cu:456-498) -- the per-sample fast loop's values
+// and order, so its bits.  sphere_sample_texel: one sample's source texel; sphere_fold_sample: its terms.
 template <int TEX, typename Cam>
 __device__ __forceinline__ float sphere_sample_texel(Cam& c, float4 ph, __amdgpu_buffer_rsrc_t rs, float4 rw) {
     const float dep = depth_from_plane_fast(ph, rw);
@@ -664,28 +663,12 @@ __device__ __forceinline__ void sphere_fold_sample(float w, float r, float sp, f
     sss = fmaf(ws, sp, sss);
 }
 
-// sample(s, rw, r): sample s's (ray, w) and reference texel, from the staged patch
-template <int TEX, typename Cam, typename SampleF>
-__device__ __forceinline__ void sphere_view_sums(Cam& c, float4 ph, __amdgpu_buffer_rsrc_t rs, SampleF&& sample,
-                                                 f32x2& ssrs, float& sss) {
-    ssrs = splat2(0.f);
-    sss = 0.f;
-#pragma nounroll
-    for (int s = 0; s < 36; ++s) {
-        float4 rw;
-        float r;
-        sample(s, rw, r);
-        sphere_fold_sample(rw.w, r, sphere_sample_texel<TEX>(c, ph, rs, rw), ssrs, sss);
-    }
-}
-
 // fixkey: k_eval_nb's (pixel << 8 | hypothesis << 5) for deferring interpolation fallbacks to k_nb_fix;
-// kFixInline: the fallback runs inline (k_eval_nb / the test hook without a queue); kFixNone (the
-// default): no fallback -- the refinement kernels' interpolated instances (V > 4), whose inline fallbacks
-// cost C3 6.6 ms per half-sweep (random candidates; profiles/r04_prof_ab.txt) and which the float64 study
-// finds within 1e-4 on every pole / seam / random query tried from 2000x1000 up except pole-straddling
-// patches (k_eval_nb, which takes the most hypotheses, keeps the fallback)
-constexpr uint32_t kFixNone = ~0u, kFixInline = ~0u - 1u;
+// kFixNone (the default): no fallback -- the refinement kernels' interpolated instances (V > 4), whose
+// inline fallbacks cost C3 6.6 ms per half-sweep (random candidates; profiles/r04_prof_ab.txt) and which
+// the float64 study finds within 1e-4 on every pole / seam / random query tried from 2000x1000 up except
+// pole-straddling patches (k_eval_nb, which takes the most hypotheses, keeps the fallback)
+constexpr uint32_t kFixNone = ~0u;
 template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM = 0, bool FULL = false>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv_rt, float (&cost)[VB],
@@ -909,44 +892,31 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 column(4, c4);
                 __builtin_amdgcn_sched_barrier(0);           // one view's nodes live at a time
             }
-            // Lanes whose corners spread too far take the view with every sample projected (the
-            // !interp_done loop's arithmetic and order).  In k_eval_nb (fixkey set) they are queued for
-            // k_nb_fix instead, which recomputes those (pixel, hypothesis, view) costs the same way after
-            // the launch: done here, one such lane made its whole wave run the 36 projections (3-6% of
-            // lanes, so most waves: k_eval_nb +28%).  The inline form stays for the test hook and a full
-            // queue.  After the view loop, with no node live (inside it the queue's code spilled).
+            // Lanes whose corners spread too far go to k_nb_fix's queue (fixkey set: k_eval_nb and its test
+            // hook), which recomputes those (pixel, hypothesis, view) costs with every sample projected --
+            // the per-sample fast arithmetic bit for bit -- after the launch.  Done here, one such lane made its
+            // whole wave run the 36 projections (3-6% of lanes, so most waves: k_eval_nb +28%).  After the
+            // view loop, with no node live (inside it the queue's code spilled).  The queue holds every
+            // entry a launch can produce (capi.cpp sizes it), so none is dropped.
+            if (fixkey != kFixNone) {
 #pragma unroll
-            for (int v = 0; v < VB; ++v) {
-                if (!has(v) || fixkey == kFixNone) continue;
-                bool redo = (rough >> v) & 1u;
-                if (fixkey != kFixInline) {
+                for (int v = 0; v < VB; ++v) {
+                    if (!has(v)) continue;
+                    const bool redo = (rough >> v) & 1u;
                     const unsigned long long b = __ballot(redo);
                     if (b) {
                         const int lane = __lane_id();
                         const int leader = __ffsll(static_cast<long long>(b)) - 1;
                         unsigned base = 0u;
-                        // one of kNbFixRegions counters per block (a single one serialised the atomics: k_eval_nb
-                        // +0.35 ms at the metric)
+                        // one of kNbFixRegions counters per block (a single one serialised the atomics:
+                        // k_eval_nb +0.35 ms at the metric)
                         const unsigned region = blockIdx.x % kNbFixRegions;
                         if (lane == leader) base = atomicAdd(kp.nbfix_count + region, static_cast<unsigned>(__popcll(b)));
                         base = __shfl(base, leader);
                         const unsigned slot = base + static_cast<unsigned>(__popcll(b & ((1ull << lane) - 1ull)));
-                        if (redo && slot < kp.nbfix_cap) {
+                        if (redo && slot < kp.nbfix_cap)
                             kp.nbfix[static_cast<long long>(region) * kp.nbfix_cap + slot] = fixkey | static_cast<uint32_t>(cv[v] - 1);
-                            redo = false;
-                        }
                     }
-                }
-                if (redo) {
-                    ConstCam& c = PCV(v);
-                    const __amdgpu_buffer_rsrc_t rs =
-                        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000);
-                    sphere_view_sums<TEX>(c, ph, rs, [&](int s, float4& rw, float& r) {
-                        const int jj = s - (s / 6) * 6;
-                        const float4 q = pt.rw[s * pt.stride];
-                        rw = make_float4(q.x, pt.rr[jj * pt.stride], q.y, q.z);
-                        r = q.w;
-                    }, ssrs[v], sss[v]);
                 }
             }
         }
@@ -1714,7 +1684,6 @@ constexpr int nb_vb() {
     return VB > cap ? cap : VB;
 }
 constexpr int kNbLanes = 8;                 // the 8 neighbour directions (the current plane's costs are cached)
-constexpr int kNbPix = 32;                  // pixels per 256-lane block
 
 static inline size_t nb_lds_bytes(int model, int S, int nside, int npix = kNbPix) {
     return model == kSphere ? (sizeof(float4) * S + sizeof(float) * nside) * npix
@@ -1807,17 +1776,14 @@ __device__ __forceinline__ Patch coop_patch_sep(const KParams& kp, bool valid, i
 constexpr bool kRefPipe = true;
 template <int MODEL, int VB>
 constexpr int ref_vb() { return (VB == 4 || (VB > 4 && MODEL == kSphere)) ? 2 : (VB > kEvalVB ? kEvalVB : VB); }
-#ifndef ACMMP_REF_PIN_VB
-#define ACMMP_REF_PIN_VB 4
-#endif
-// k_eval_ref's chunk: the fast pinhole chunks' homogeneous points hold ~12 VGPRs per view across the sample loop
+// k_eval_ref's chunk: the fast pinhole chunks' homogeneous points hold ~12 VGPRs per view across the sample
+// loop, so 4-view chunks took 162 VGPRs (3 waves per SIMD) and 2-view ones take 100 (5 waves): C2 k_eval_ref
+// 1.90 -> 1.85 ms, +1% (profiles/r04_ab4_ab.txt).  (Capping the SPHERE V > 4 instance at 5 waves instead,
+// 120 -> 96 VGPRs, lost 5% of C3's k_eval_ref there.)
 template <int MODEL, int VB, int TF>
 constexpr int ref_vb_eval() {
-    return (MODEL == kPinhole && TF == 2 && ref_vb<MODEL, VB>() > ACMMP_REF_PIN_VB) ? ACMMP_REF_PIN_VB : ref_vb<MODEL, VB>();
+    return (MODEL == kPinhole && TF == 2 && ref_vb<MODEL, VB>() > 2) ? 2 : ref_vb<MODEL, VB>();
 }
-#ifndef ACMMP_REF_WAVES
-#define ACMMP_REF_WAVES 1
-#endif
 constexpr int kRefLanes = 5;                // refinement candidates (ACMMP.cu:870)
 constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 lanes used)
 constexpr int kRefSlots = kRefPix * kRefLanes;  // survivor slots per k_eval_ref block
@@ -1843,8 +1809,10 @@ __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour
 // own register allocation (a runtime branch between them sized every variant for the largest: 23
 // VGPRs spilled at the 64-VGPR budget; r02 A/B profiles/r02_split_nb_ab.txt: fast 388 -> 394, exact
 // 316.6 -> 320 Mpixel-iterations/s)
+// fast pinhole: 6 waves (80 VGPRs, 5 dwords spilled outside the sample loops) against 5 unconstrained (90):
+// C2 k_eval_nb 3.233 -> 3.212 ms (profiles/r04_ab5_ab.txt)
 template <int MODEL, int VB, int TEX, int FM>
-__global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? 7 : 8) : 1) void k_eval_nb(
+__global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? 7 : 8) : (FM ? 6 : 1)) void k_eval_nb(
     const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
@@ -1866,7 +1834,7 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? 7 : 8) : 1) void k_ev
     const float4 ph = plane_at(kp, pos);
     const uint32_t all = kp.nb_views;
     float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
-    const uint32_t fixkey = kp.nbfix ? (static_cast<uint32_t>(ci) << 8) | (static_cast<uint32_t>(h) << 5) : kFixInline;
+    const uint32_t fixkey = kp.nbfix ? (static_cast<uint32_t>(ci) << 8) | (static_cast<uint32_t>(h) << 5) : kFixNone;
     for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
         kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; }, fixkey);
 }
@@ -1978,7 +1946,7 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
     };
 
     // ---- joint view selection :1146-1208
-    constexpr int VMAX = VB < 8 ? VB : kMaxViews;            // pick_vb: V <= VB when VB < 8
+    constexpr int VMAX = VB;                                 // launch_select: V <= VB (1, 2, 4, 8, 16 or 32)
     // up to 4 views the 8 x V cost matrix is read once into registers (all loads in flight together)
     // and both passes over it below use it; wider launches re-read it from L2
     constexpr bool kRegCost = VMAX <= 4;
@@ -2281,7 +2249,7 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
 
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
 template <int MODEL, int VB, bool GEOM, int TF>
-__global__ __launch_bounds__(256, ACMMP_REF_WAVES) void k_eval_ref(const KParams kp, const int colour) {
+__global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
@@ -2767,7 +2735,7 @@ hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s);
 // profiles/r02_view_chunk_ab.txt: SPHERE V = 15 at 3200x1600 +3.7%, at 4096x2048 +6.4%; pinhole V = 10
 // at 1600x1200, 77 MB of texels, -1% -- not chunked).  ACMMP_NB_VIEW_CHUNK=c overrides (c <= 0: one
 // launch over all views); read per half-sweep.
-static int nb_view_chunk(const KParams& kp) {
+int nb_view_chunk(const KParams& kp) {
     const char* e = std::getenv("ACMMP_NB_VIEW_CHUNK");
     int c = e ? std::atoi(e) : 0;
     if (!e) {
@@ -2785,7 +2753,7 @@ hipError_t launch_eval_nb(const KParams& kp0, int colour, hipStream_t s) {
     if (!fix) kp.nbfix = nullptr;
     hipError_t e0 = hipSuccess;
     if (fix && (e0 = hipMemsetAsync(kp.nbfix_count, 0, sizeof(unsigned) * kNbFixRegions, s)) != hipSuccess) return e0;
-    const int chunk = nb_view_chunk(kp);
+    const int chunk = kp.nb_chunk;                          // nb_view_chunk, fixed when the run's KParams were built
     for (int v0 = 0; v0 < kp.V; v0 += chunk) {
         const int v1 = std::min(kp.V, v0 + chunk);
         const uint32_t hi = v1 >= 32 ? 0xFFFFFFFFu : ((1u << v1) - 1u);
@@ -2822,7 +2790,7 @@ __global__ __launch_bounds__(256) void k_debug_nb(const KParams kp, int n, const
     const float4 ph = planes[k];
     float* o = out + k * kp.V;
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
-    const uint32_t fixkey = kp.nbfix ? (static_cast<uint32_t>(q) << 8) | (static_cast<uint32_t>(h) << 5) : kFixInline;
+    const uint32_t fixkey = kp.nbfix ? (static_cast<uint32_t>(q) << 8) | (static_cast<uint32_t>(h) << 5) : kFixNone;
     for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
         kp, px, py, pt, ph, all, [&](int v, float c) { o[v] = c; }, fixkey);
 }
@@ -2858,10 +2826,13 @@ __global__ __launch_bounds__(256) void k_debug_nb_fix(const KParams kp, const in
 
 hipError_t launch_debug_nb(const KParams& kp0, int n, const int* px, const int* py, const float4* planes, float* out,
                            hipStream_t s) {
-    // the hook takes k_eval_nb's path, deferred fallbacks included (ACMMP_NB_FIX=0: inline)
+    // the hook takes k_eval_nb's path, deferred fallbacks included
     KParams kp = kp0;
     const bool fix = kp.nbfix && kp.model == kSphere && kp.fast && kp.tex16 && kp.interp && n < (1 << 24);
     if (!fix) kp.nbfix = nullptr;
+    // the queue holds every entry: a region's blocks x 256 lanes x all V views (one launch here)
+    if (fix && static_cast<long long>(cdiv(cdiv(n, kNbPix), kNbFixRegions)) * 256 * kp.V > kp.nbfix_cap)
+        return hipErrorInvalidValue;
     hipError_t e0 = hipSuccess;
     if (fix && (e0 = hipMemsetAsync(kp.nbfix_count, 0, sizeof(unsigned) * kNbFixRegions, s)) != hipSuccess) return e0;
     const size_t lds_nb = nb_lds_bytes(kp.model, kp.S, kp.nside);
@@ -2895,8 +2866,28 @@ hipError_t launch_eval_nb_views(const KParams& kp, int colour, hipStream_t s) {
 #if ACMMP_IN_TU(3)
 hipError_t launch_select(const KParams& kp, int colour, int iter, hipStream_t s) {
     const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
-    if (kp.geom) ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, true><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
-    else ACMMP_DISPATCH(kp.model, kp.V, (k_select<M, VBC, false><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter)));
+    // the per-view arrays of k_select are sized to the next power of two of V: a 32-entry bound for every V
+    // above 4 kept C3's (V = 15) probabilities in 384 B of scratch per lane
+    const int vs = kp.V <= 4 ? pick_vb(kp.V) : (kp.V <= 8 ? 8 : (kp.V <= 16 ? 16 : 32));
+#define ACMMP_SELECT(MV)                                                                                              \
+    do {                                                                                                              \
+        if (kp.model == kSphere) {                                                                                    \
+            if (kp.geom) k_select<kSphere, MV, true><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter);               \
+            else k_select<kSphere, MV, false><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter);                      \
+        } else {                                                                                                      \
+            if (kp.geom) k_select<kPinhole, MV, true><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter);              \
+            else k_select<kPinhole, MV, false><<<cdiv(npix, 256), 256, 0, s>>>(kp, colour, iter);                     \
+        }                                                                                                             \
+    } while (0)
+    switch (vs) {
+        case 1: ACMMP_SELECT(1); break;
+        case 2: ACMMP_SELECT(2); break;
+        case 4: ACMMP_SELECT(4); break;
+        case 8: ACMMP_SELECT(8); break;
+        case 16: ACMMP_SELECT(16); break;
+        default: ACMMP_SELECT(32); break;
+    }
+#undef ACMMP_SELECT
     return hipGetLastError();
 }
 #endif  // ACMMP_IN_TU(3)

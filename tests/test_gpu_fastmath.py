@@ -272,20 +272,22 @@ def test_fast_mode_is_deterministic(ctx):
     assert np.array_equal(a[0], b[0], equal_nan=True) and np.array_equal(a[1], b[1], equal_nan=True)
 
 
-@pytest.mark.parametrize("shape,spread", [((2000, 1500, 4), "256"), ((2000, 1000, 6), "256"), ((2000, 1000, 4), "8")])
-def test_deferred_interpolation_fallbacks_are_bit_identical(ctx, shape, spread, monkeypatch):
-    """k_eval_nb queues the lanes whose interpolation nodes spread too far (ncc_chunk) and k_nb_fix recomputes
-    those costs after the launch; inline (ACMMP_NB_FIX=0) the lane does the same arithmetic itself.  Both
-    must give the same run bit for bit -- a full fast-mode RunPatchMatch at interpolating sizes, with the
-    product threshold and with a small one (most lanes fall back)."""
+@pytest.mark.parametrize("shape", [(2000, 1500, 4), (2000, 1000, 4)])
+def test_deferred_interpolation_fallbacks_are_per_sample_bit_exact(ctx, shape, monkeypatch):
+    """k_eval_nb queues the (pixel, hypothesis, view) entries whose interpolation nodes spread too far
+    (ncc_chunk) and k_nb_fix recomputes them with every sample projected.  With ACMMP_SPREAD_MAX=-1 every entry
+    falls back, so a full fast-mode RunPatchMatch must be the per-sample fast run (ACMMP_INTERP=0) bit for bit
+    -- at V = 4, where only k_eval_nb interpolates (k_eval_ref's V > 4 instances interpolate too)."""
     W, H, V = shape
     sc = scene.sphere_scene(W, H, n_src=V, seed=71, n_waves=16)
     setup = plain_setup(sc, params_for(sc))
-    monkeypatch.setenv("ACMMP_SPREAD_MAX", spread)
+    monkeypatch.setenv("ACMMP_SPREAD_MAX", "-1")
     a = run(ctx, "fast", 5, setup=setup)
-    monkeypatch.setenv("ACMMP_NB_FIX", "0")
-    b = run(ctx, "fast", 5, setup=setup)
-    monkeypatch.delenv("ACMMP_NB_FIX")
     monkeypatch.delenv("ACMMP_SPREAD_MAX")
+    monkeypatch.setenv("ACMMP_INTERP", "0")
+    b = run(ctx, "fast", 5, setup=setup)
+    monkeypatch.delenv("ACMMP_INTERP")
+    c = run(ctx, "fast", 5, setup=setup)
     np.testing.assert_array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
     np.testing.assert_array_equal(a[1].view(np.uint32), b[1].view(np.uint32))
+    assert not np.array_equal(c[1].view(np.uint32), b[1].view(np.uint32))     # the product interpolates

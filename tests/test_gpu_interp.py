@@ -206,10 +206,12 @@ def test_pinhole_homogeneous_k_eval_nb_per_query(ctx, name, monkeypatch):
 
 
 @pytest.mark.parametrize("name", list(CONFIGS))
-def test_deferred_fallbacks_per_query_bit_identical(ctx, name, monkeypatch):
-    """acmmp_debug_ncc_nb runs k_eval_nb's path including the deferred interpolation fallbacks (queued in
-    ncc_chunk, recomputed by k_debug_nb_fix like k_nb_fix); inline (ACMMP_NB_FIX=0) the lane recomputes them
-    itself.  The same costs bit for bit on the pole / seam / random query sets."""
+def test_deferred_fallbacks_are_per_sample_bit_exact(ctx, name, monkeypatch):
+    """acmmp_debug_ncc_nb runs k_eval_nb's path including the deferred interpolation fallbacks (ncc_chunk
+    queues a (pixel, hypothesis, view) whose nodes spread too far; k_debug_nb_fix recomputes it with k_nb_fix's
+    code).  A recomputed cost is the per-sample fast NCC (acmmp_debug_ncc) bit for bit.  With the product
+    threshold on the pole / seam / random sets, and with ACMMP_SPREAD_MAX=-1, where every entry falls back --
+    then every cost must equal the per-sample hook's."""
     make, _ = CONFIGS[name]
     sc = make()
     c0 = sc.cameras[0]
@@ -222,24 +224,17 @@ def test_deferred_fallbacks_per_query_bit_identical(ctx, name, monkeypatch):
         px, py, _ = ni.special_pixels(sc, kind, n, seed=len(kind) + 17)
         planes = ni.near_surface_planes(sc, px, py, 8, seed=len(kind) + 29)
         planes[:, 4:] = ni.near_surface_planes(sc, px, py, 4, seed=len(kind) + 31, spread=1.5, depth_jitter=0.4)
-        for spread in ("256", "4"):   # the product threshold; a small one so that most lanes fall back
-            monkeypatch.setenv("ACMMP_SPREAD_MAX", spread)
-            ctx.set_params(p)
-            queued = ctx.debug_ncc_nb(px, py, planes)
-            monkeypatch.setenv("ACMMP_NB_FIX", "0")
-            ctx.set_params(p)
-            inline = ctx.debug_ncc_nb(px, py, planes)
-            monkeypatch.delenv("ACMMP_NB_FIX")
-            bad = np.nonzero(queued.view(np.uint32) != inline.view(np.uint32))
-            assert bad[0].size == 0, (kind, spread, bad[0].size,
-                                      [(int(a), int(b), int(c), float(queued[a, b, c]), float(inline[a, b, c]))
-                                       for a, b, c in zip(*bad)][:5])
-        # the small threshold did send lanes to the fallback: their costs are the per-sample ones, not the
-        # interpolated ones
-        monkeypatch.setenv("ACMMP_SPREAD_MAX", "1e30")
+        ps = ctx.debug_ncc(np.repeat(px, 8), np.repeat(py, 8), planes.reshape(-1, 4)).reshape(len(px), 8, -1)
+        monkeypatch.setenv("ACMMP_SPREAD_MAX", "-1")
         ctx.set_params(p)
-        interp_only = ctx.debug_ncc_nb(px, py, planes)
+        every = ctx.debug_ncc_nb(px, py, planes)
         monkeypatch.delenv("ACMMP_SPREAD_MAX")
         ctx.set_params(p)
-        assert np.mean(interp_only.view(np.uint32) != queued.view(np.uint32)) > 0.2, kind
+        product = ctx.debug_ncc_nb(px, py, planes)
+        bad = np.nonzero(every.view(np.uint32) != ps.view(np.uint32))
+        assert bad[0].size == 0, (kind, bad[0].size, [(int(a), int(b), int(c), float(every[a, b, c]), float(ps[a, b, c]))
+                                                      for a, b, c in zip(*bad)][:5])
+        # the product's costs: interpolated or, where it fell back, the per-sample ones (and the interpolation
+        # does not equal the per-sample arithmetic everywhere, so the comparison above tested the queue)
+        assert np.mean(product.view(np.uint32) != ps.view(np.uint32)) > 0.2, kind
     ctx.set_math("exact")
