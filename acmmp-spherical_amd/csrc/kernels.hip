@@ -2398,7 +2398,17 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
         pt.sbw = ps.x; pt.sref = ps.y; pt.srr = ps.z; pt.center = ps.w;
         float temp_cost = kp.cand_cost[h * Pc + ci];
         float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
-        constexpr int VBT = ref_vb<MODEL, VB>();
+        // SPHERE V > 4: 4-view chunks (87 VGPRs, 5 waves) -- each chunk recomputes the 36 samples' rays,
+        // weights and reference texels, so fewer chunks save that work: C3 k_eval_ref + tail 10.52 -> 9.03 ms
+        // against 2-view chunks (74 VGPRs, 6 waves), +5.4% (profiles/r04_ab6_ab.txt)
+#ifndef ACMMP_TAIL_SPH_VB
+#define ACMMP_TAIL_SPH_VB 4
+#endif
+#ifndef ACMMP_TAIL_PIN_VB
+#define ACMMP_TAIL_PIN_VB 4
+#endif
+        constexpr int VBT = (MODEL == kSphere && VB > 4) ? ACMMP_TAIL_SPH_VB
+                          : (MODEL == kPinhole && VB > 4) ? ACMMP_TAIL_PIN_VB : ref_vb<MODEL, VB>();
         for_all_views_tf<MODEL, VBT, 0, kRefPipe, TF>(kp, px, py, pt, tp, umask, [&](int v, float c) {
             vcost[v * Pc] = c;
             const float w = vw_get(vwp, v);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # BASELINE.json's other single-GPU configurations: RunPatchMatch bench lines (C2 1600x1200 pinhole V=10,
 # C3 at the 3200x1600 the reference scheduler runs 4096x2048 inputs at, V=15), their PMC passes, and the
-# C2 / C3 ProcessProblem schedules.  Usage (GPU box, repo root): bash scripts/r03_configs.sh TAG [no-pmc]
+# C2 / C3 ProcessProblem schedules.  Usage (GPU box, repo root): bash scripts/configs.sh TAG [no-pmc]
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-configs}

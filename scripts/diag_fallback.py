@@ -1,6 +1,7 @@
-"""Which interpolation fallback is the per-sample fast arithmetic?  Per query (acmmp_debug_ncc_nb) at the
-metric view: queued (k_debug_nb_fix) and inline fallbacks at a small spread threshold, the interpolation
-alone, against the per-sample fast hook (acmmp_debug_ncc) -- bitwise agreement and max |d|."""
+"""Per query (acmmp_debug_ncc_nb) at the metric view: k_eval_nb's path with every entry deferred
+(ACMMP_SPREAD_MAX=-1), a small threshold, the product one and the interpolation alone, against the
+per-sample fast hook (acmmp_debug_ncc) -- bitwise agreement and max |d|.  (Round 4 found the deleted inline
+fallback wrong on 22% of forced random queries this way.)"""
 import os
 import sys
 
@@ -23,10 +24,9 @@ for kind in ("random", "pole"):
     px, py, _ = ni.special_pixels(sc, kind, 40, seed=len(kind) + 17)
     planes = ni.near_surface_planes(sc, px, py, 8, seed=len(kind) + 29)
     res = {}
-    for tag, env in (("queue4", {"ACMMP_SPREAD_MAX": "4"}), ("inline4", {"ACMMP_SPREAD_MAX": "4", "ACMMP_NB_FIX": "0"}),
-                     ("interp", {"ACMMP_SPREAD_MAX": "1e30"}), ("queue256", {}), ("inline256", {"ACMMP_NB_FIX": "0"})):
-        for k in ("ACMMP_SPREAD_MAX", "ACMMP_NB_FIX"):
-            os.environ.pop(k, None)
+    for tag, env in (("queue-all", {"ACMMP_SPREAD_MAX": "-1"}), ("queue4", {"ACMMP_SPREAD_MAX": "4"}),
+                     ("interp", {"ACMMP_SPREAD_MAX": "1e30"}), ("queue256", {})):
+        os.environ.pop("ACMMP_SPREAD_MAX", None)
         os.environ.update(env)
         ctx.set_params(p)
         res[tag] = ctx.debug_ncc_nb(px, py, planes)

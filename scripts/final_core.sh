@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-3 record of the committed tree (GPU box, repo root): parity tests, PMC passes of the headline
+# Record of the committed tree (GPU box, repo root): parity tests, PMC passes of the headline
 # config (their summary feeds the bench line's `traffic`), the default bench line, a rocprofv3 kernel trace
 # of the same timed region (bench.py --timed-only, 20 steps so that the warmup's dispatches weigh little in
-# rocprof's all-dispatch mean) with trace_window.py's recomputed frac, then scripts/r03_configs.sh (C2 / C3
-# PMC, bench lines and the C2 schedule).  Usage: bash scripts/r03_final.sh TAG
+# rocprof's all-dispatch mean) with trace_window.py's recomputed frac, then scripts/configs.sh (C2 / C3
+# PMC, bench lines and the C2 schedule).  Usage: bash scripts/final_core.sh TAG
 set -o pipefail
 TAG=${1:-final}
 OUT=gpurun_out/$TAG
@@ -18,5 +18,5 @@ timeout -k 10 600 python bench.py --pmc $OUT/pmc_propagate.json > $OUT/bench.jso
 cut -c1-400 $OUT/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --timed-only --steps 20 $Q --pmc $OUT/pmc_propagate.json > $OUT/prof_bench.json 2> $OUT/prof.err || { echo "rocprof failed"; tail -20 $OUT/prof.err; exit 1; }
 python scripts/trace_window.py $OUT/prof/run_kernel_trace.csv $OUT/prof_bench.json --json $OUT/trace_window.json || exit 1
-bash scripts/r03_configs.sh $TAG/cfg || exit 1
+# (configs: scripts/configs.sh, a call of its own)
 echo FINAL_DONE
