@@ -881,13 +881,18 @@ static unsigned long long colour_pixels(const acmmp_ctx* c, const KParams& kp, i
 // S = 4 beats 6 / 8 / 12 by 1-4%); 0 (no split) for one view, for colour grids too large for the 32-bit
 // queue entries, or with ACMMP_REF_SPLIT=0 in the environment (A/B switch).
 // Read at every run (one getenv per RunPatchMatch), so tests can switch it within one process.
-static int ref_split_point(int V, size_t Pc) {
+// interp_ref: the refinement's first part interpolates SPHERE sample coordinates (fast mode, V > 4, views
+// of the interpolation's size), which makes its views cheaper than the tail's per-sample ones: S = 8 there
+// from V = 9 up (C3 V = 15: 88.9 -> 90.4 Mpix-it/s against S = 4; S = 10 / 12 lose, and the exact mode
+// loses 5% at S = 8, profiles/r04_split_ab.txt, r04_split2_ab.txt)
+static int ref_split_point(int V, size_t Pc, bool interp_ref) {
     const char* e_on = std::getenv("ACMMP_REF_SPLIT");
     const char* e_at = std::getenv("ACMMP_REF_SPLIT_AT");  // ACMMP_REF_SPLIT_AT=S: fixed split (A/B)
     const int enabled = e_on ? std::atoi(e_on) : 1;
     const int at = e_at ? std::atoi(e_at) : 0;
     if (!enabled || V < 2 || Pc >= (static_cast<size_t>(1) << 29)) return 0;
     if (at > 0) return at < V ? at : 0;
+    if (interp_ref && V > 8) return 8;
     return V <= 4 ? V / 2 : 4;
 }
 
@@ -1025,7 +1030,7 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.surv_pre = reinterpret_cast<unsigned*>(c->d_scratch + off[14]);
     kp.surv_dense = reinterpret_cast<uint32_t*>(c->d_scratch + off[15]);
     kp.nbfix_cap = static_cast<unsigned>(fix_cap);
-    kp.ref_split = ref_split_point(kp.V, Pc);
+    kp.ref_split = ref_split_point(kp.V, Pc, kp.model == kSphere && kp.fast && kp.tex16 && kp.interp && kp.V > 4);
     if (!c->d_work) HIP_TRY(c, dalloc(c->d_work, 256));
     kp.work = c->d_work;
     kp.nb_views = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);

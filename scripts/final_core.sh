@@ -12,6 +12,8 @@ export TMPDIR=/tmp
 Q="--no-cpu-baseline --no-variant --no-pipeline --no-other-mode"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -rA > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|ERROR" $OUT/pytest_gpu.log | head -5; tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -1 $OUT/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; }
+tail -2 $OUT/smoke.log
 bash scripts/pmc.sh $OUT/pmc "--steps 1 --warmup 1 --timed-only $Q" || exit 1
 python scripts/pmc_summary.py $OUT/pmc --json $OUT/pmc_propagate.json > $OUT/pmc_summary.txt || exit 1
 timeout -k 10 600 python bench.py --pmc $OUT/pmc_propagate.json > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
