@@ -1812,7 +1812,10 @@ __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour
 // fast pinhole: 6 waves (80 VGPRs, 5 dwords spilled outside the sample loops) against 5 unconstrained (90):
 // C2 k_eval_nb 3.233 -> 3.212 ms (profiles/r04_ab5_ab.txt)
 template <int MODEL, int VB, int TEX, int FM>
-__global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? 7 : 8) : (FM ? 6 : 1)) void k_eval_nb(
+#ifndef ACMMP_NB_SPH_WAVES
+#define ACMMP_NB_SPH_WAVES 7
+#endif
+__global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_SPH_WAVES : 8) : (FM ? 6 : 1)) void k_eval_nb(
     const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;

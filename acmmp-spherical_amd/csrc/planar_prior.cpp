@@ -71,6 +71,8 @@ public:
         p_.push_back({-M, -M});
         p_.push_back({3 * M, -M});
         p_.push_back({-M, 3 * M});
+        t_.reserve(2 * static_cast<size_t>(n_real_) + 16);        // a triangulation of n points: < 2n + 1 triangles
+        mark_.reserve(t_.capacity());
         t_.push_back({{n_real_, n_real_ + 1, n_real_ + 2}, {-1, -1, -1}, true});
     }
 
@@ -92,17 +94,26 @@ public:
 
     // triangles without super vertices, each rotated to start at its lowest point index (orientation
     // kept) and listed in increasing (v0, v1, v2): an order that depends on the triangle set only
+    // (a counting sort on v0, then the few triangles sharing a v0 by (v1, v2): std::sort of the whole list
+    // took 12-17 ms of a 2000x1500 view's 65)
     std::vector<std::array<int, 3>> triangles() const {
-        std::vector<std::array<int, 3>> out;
+        std::vector<int> start(static_cast<size_t>(n_real_) + 1, 0);
         for (const Tri& t : t_) {
-            if (!t.alive) continue;
-            if (t.v[0] >= n_real_ || t.v[1] >= n_real_ || t.v[2] >= n_real_) continue;
+            if (!t.alive || t.v[0] >= n_real_ || t.v[1] >= n_real_ || t.v[2] >= n_real_) continue;
+            ++start[std::min(t.v[0], std::min(t.v[1], t.v[2])) + 1];
+        }
+        for (int i = 0; i < n_real_; ++i) start[i + 1] += start[i];
+        std::vector<std::array<int, 3>> out(static_cast<size_t>(start[n_real_]));
+        std::vector<int> fill(start.begin(), start.end() - 1);
+        for (const Tri& t : t_) {
+            if (!t.alive || t.v[0] >= n_real_ || t.v[1] >= n_real_ || t.v[2] >= n_real_) continue;
             int r = 0;
             if (t.v[1] < t.v[r]) r = 1;
             if (t.v[2] < t.v[r]) r = 2;
-            out.push_back({t.v[r], t.v[(r + 1) % 3], t.v[(r + 2) % 3]});
+            out[fill[t.v[r]]++] = {t.v[r], t.v[(r + 1) % 3], t.v[(r + 2) % 3]};
         }
-        std::sort(out.begin(), out.end());
+        for (int i = 0; i < n_real_; ++i)
+            if (start[i + 1] - start[i] > 1) std::sort(out.begin() + start[i], out.begin() + start[i + 1]);
         return out;
     }
 
