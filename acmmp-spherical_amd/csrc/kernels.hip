@@ -2334,26 +2334,43 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
 // k_eval_ref's per-block survivor counts -> their exclusive prefix surv_pre[0 .. nref] (surv_pre[nref] =
 // all survivors): one block, each thread a contiguous run of k_eval_ref blocks.
 __global__ __launch_bounds__(1024) void k_tail_scan(const KParams kp, const int nref) {
+    // 8192 counts per pass staged in LDS with coalesced loads (a contiguous run per thread read straight from
+    // HBM kept one load in flight per thread: 39 us at the metric, profiles/r04_final_kernel_stats.csv)
+    constexpr int kPass = 8192, kPer = kPass / 1024;
+    __shared__ unsigned cnt[kPass];
     __shared__ unsigned part[1024];
     const int t = threadIdx.x;
-    const int per = (nref + 1023) / 1024;
-    const int b0 = min(nref, t * per), b1 = min(nref, b0 + per);
-    unsigned sum = 0u;
-    for (int b = b0; b < b1; ++b) sum += kp.surv_count[b];
-    part[t] = sum;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {               // inclusive scan of the 1024 run sums
-        const unsigned add = t >= off ? part[t - off] : 0u;
+    unsigned carry = 0u;
+    for (int base = 0; base < nref; base += kPass) {
+        const int m = min(kPass, nref - base);
+        for (int i = t; i < m; i += 1024) cnt[i] = kp.surv_count[base + i];
         __syncthreads();
-        part[t] += add;
+        unsigned v[kPer], sum = 0u;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            v[k] = t * kPer + k < m ? cnt[t * kPer + k] : 0u;
+            sum += v[k];
+        }
+        part[t] = sum;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {           // inclusive scan of the 1024 run sums
+            const unsigned add = t >= off ? part[t - off] : 0u;
+            __syncthreads();
+            part[t] += add;
+            __syncthreads();
+        }
+        unsigned acc = carry + part[t] - sum;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {                     // exclusive prefix, in place
+            cnt[t * kPer + k] = acc;
+            acc += v[k];
+        }
+        carry += part[1023];
+        __syncthreads();
+        for (int i = t; i < m; i += 1024) kp.surv_pre[base + i] = cnt[i];
         __syncthreads();
     }
-    unsigned acc = part[t] - sum;
-    for (int b = b0; b < b1; ++b) {
-        kp.surv_pre[b] = acc;
-        acc += kp.surv_count[b];
-    }
-    if (t == 1023) kp.surv_pre[nref] = part[1023];
+    if (t == 0) kp.surv_pre[nref] = carry;
 }
 
 // The survivors in k_eval_ref block order, dense: block b's slots to surv_dense[surv_pre[b] ...].
