@@ -1813,7 +1813,7 @@ __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour
 // C2 k_eval_nb 3.233 -> 3.212 ms (profiles/r04_ab5_ab.txt)
 template <int MODEL, int VB, int TEX, int FM>
 #ifndef ACMMP_NB_SPH_WAVES
-#define ACMMP_NB_SPH_WAVES 7
+#define ACMMP_NB_SPH_WAVES 7   // 6: no spills (writes 0.49 -> 0.20 GB per launch) but +3% time, profiles/r04_ab8_ab.txt
 #endif
 __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_SPH_WAVES : 8) : (FM ? 6 : 1)) void k_eval_nb(
     const KParams kp, const int colour) {
