@@ -858,13 +858,14 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                     }
                 }
                 // The interpolation holds where the source mapping is smooth over the patch.  Where the four
-                // corner nodes spread over more than kp.spread_max source pixels in x or y -- a patch landing
-                // next to a source pole (longitude stretches as 1 / cos(latitude)) or a near-grazing plane
-                // whose depth flips sign inside the patch -- the lane projects all 36 samples instead, in the
-                // per-sample loop's order and arithmetic (so those costs are the per-sample fast ones bit for
-                // bit).  float64 study (tests/np_interp.py, tests/test_interp_design.py): with the test, the
-                // interpolated NCC stays within 4e-5 of the projected one on every query tried from 1600x800
-                // up, pole-adjacent and random planes included; without it the tail reached 0.6.
+                // corner nodes spread over more than kp.spread_max (256) source pixels in x or y -- a patch
+                // landing next to a source pole (longitude stretches as 1 / cos(latitude)) or a near-grazing
+                // plane whose depth flips sign inside the patch -- the (pixel, hypothesis, view) goes to
+                // k_nb_fix, which projects all 36 samples in the per-sample loop's order and arithmetic (so
+                // those costs are the per-sample fast ones bit for bit).  float64 study (tests/np_interp.py,
+                // tests/test_interp_design.py): with the test, the interpolated NCC stays within 1e-4 of the
+                // projected one on every query tried from 2000x1000 up (capi.cpp's size gate), pole-adjacent
+                // and random planes included; without it the tail reached 0.6.
                 const float sx_ = fmaxf(fmaxf(nd[0][3].x, nd[3][0].x), fmaxf(nd[3][3].x, 0.0f)) -
                                   fminf(fminf(nd[0][3].x, nd[3][0].x), fminf(nd[3][3].x, 0.0f));
                 const float sy_ = fmaxf(fmaxf(nd[0][0].y, nd[0][3].y), fmaxf(nd[3][0].y, nd[3][3].y)) -
