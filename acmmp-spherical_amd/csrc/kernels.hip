@@ -2764,7 +2764,8 @@ hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s);
 // View-chunked k_eval_nb: one launch per chunk of 8 source views when the sources' texels outgrow the
 // 256 MB Infinity Cache, so all waves in flight sample the same few images (r02 A/B
 // profiles/r02_view_chunk_ab.txt: SPHERE V = 15 at 3200x1600 +3.7%, at 4096x2048 +6.4%; pinhole V = 10
-// at 1600x1200, 77 MB of texels, -1% -- not chunked).  ACMMP_NB_VIEW_CHUNK=c overrides (c <= 0: one
+// at 1600x1200, 77 MB of texels, -1% -- not chunked; round 4 with the deferred fallbacks, C3: 8 views 90.2,
+// 5 89.6, one launch 89.4 Mpix-it/s, profiles/r04_chunk_ab.txt).  ACMMP_NB_VIEW_CHUNK=c overrides (c <= 0: one
 // launch over all views); read per half-sweep.
 int nb_view_chunk(const KParams& kp) {
     const char* e = std::getenv("ACMMP_NB_VIEW_CHUNK");

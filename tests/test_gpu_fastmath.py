@@ -22,7 +22,7 @@ bit-identical, so it is held to the gates DESIGN.md §2.4 states, measured in pr
   T2  After RandomInitialization every plane is identical (same RNG draws) and costs agree within 1e-3
       for >= 99.5% (pinhole) / 99% (SPHERE) of pixels; after one black half-sweep >= 99.5% (pinhole) /
       98.5% (SPHERE) of pixels hold the same plane, and the flips are near ties: their median cost gap
-      is below 1e-4.  Where the fast k_eval_nb interpolates SPHERE sample coordinates (>= 1600x800), the
+      is below 1e-4.  Where the fast k_eval_nb interpolates SPHERE sample coordinates (>= 2000x1000), the
       98.5% holds for the per-sample fast arithmetic (ACMMP_INTERP=0) and the interpolated run may hold
       at most 0.5 pt fewer same planes than it, with the same near-tie gate on its flips (the float64
       study puts the interpolation's NCC effect below 1e-4, tests/test_interp_design.py; the flips it
