@@ -27,7 +27,7 @@ EXPORTS = [
     "acmmp_set_scaled_state", "acmmp_set_planar_prior", "acmmp_run_patchmatch", "acmmp_run_patchmatch_ex",
     "acmmp_download", "acmmp_download_aux", "acmmp_device_outputs", "acmmp_synchronize", "acmmp_last_timing",
     "acmmp_last_kernel_timing", "acmmp_last_work", "acmmp_texel_bytes", "acmmp_set_math", "acmmp_get_math", "acmmp_jbu",
-    "acmmp_debug_ncc", "acmmp_debug_geom", "acmmp_debug_ncc_nb",
+    "acmmp_debug_ncc", "acmmp_debug_geom", "acmmp_debug_ncc_nb", "acmmp_debug_ncc_ref",
     "acmmp_support_points", "acmmp_delaunay", "acmmp_prior_plane_params", "acmmp_depth_from_plane_param",
     "acmmp_planar_prior_host", "acmmp_set_planar_prior_from_maps", "acmmp_set_planar_prior_from_state",
     "acmmp_download_planar_prior",
@@ -90,6 +90,7 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_debug_ncc.argtypes = [vp, i32, vp, vp, vp, vp]
     L.acmmp_debug_geom.argtypes = [vp, i32, vp, vp, vp, vp]
     L.acmmp_debug_ncc_nb.argtypes = [vp, i32, vp, vp, vp, vp]
+    L.acmmp_debug_ncc_ref.argtypes = [vp, i32, vp, vp, vp, vp]
     L.acmmp_support_points.argtypes = [vp, i32, i32, vp, i32, vp]
     L.acmmp_delaunay.argtypes = [vp, i32, i32, i32, vp, i32, vp]
     L.acmmp_prior_plane_params.argtypes = [vp, vp, i32, i32, vp, vp]
@@ -494,15 +495,24 @@ class Context:
     def debug_geom(self, px, py, planes):
         return self._debug(self.L.acmmp_debug_geom, px, py, planes)
 
-    def debug_ncc_nb(self, px, py, planes):
-        """k_eval_nb's own NCC (fast SPHERE >= 1600x800: interpolated coordinates) of planes (n, 8, 4) at
-        pixels (px, py) -> costs (n, 8, V)."""
+    def _debug_k(self, fn, k, px, py, planes, what):
         px = np.ascontiguousarray(px, np.int32)
         py = np.ascontiguousarray(py, np.int32)
-        pl = np.ascontiguousarray(planes, np.float32).reshape(len(px), 8, 4)
-        out = np.empty((len(px), 8, self.N - 1), np.float32)
-        self._check(self.L.acmmp_debug_ncc_nb(self.h, len(px), _p(px), _p(py), _p(pl), _p(out)), "debug_ncc_nb")
+        pl = np.ascontiguousarray(planes, np.float32).reshape(len(px), k, 4)
+        out = np.empty((len(px), k, self.N - 1), np.float32)
+        self._check(fn(self.h, len(px), _p(px), _p(py), _p(pl), _p(out)), what)
         return out
+
+    def debug_ncc_nb(self, px, py, planes):
+        """k_eval_nb's own NCC (fast SPHERE from 2000x1000 up with patch_size 11: interpolated coordinates with
+        their deferred per-sample fallbacks) of planes (n, 8, 4) at pixels (px, py) -> costs (n, 8, V)."""
+        return self._debug_k(self.L.acmmp_debug_ncc_nb, 8, px, py, planes, "debug_ncc_nb")
+
+    def debug_ncc_ref(self, px, py, planes):
+        """The refinement's NCC (k_eval_ref's instance; fast SPHERE with V > 4 at the interpolation's sizes:
+        interpolated coordinates, the tail's per-sample costs where they fall back) of planes (n, 5, 4) at
+        pixels (px, py) -> costs (n, 5, V)."""
+        return self._debug_k(self.L.acmmp_debug_ncc_ref, 5, px, py, planes, "debug_ncc_ref")
 
 
 # ---- planar-prior host side (no GPU): ACMMP.cpp:904-1011, main.cpp:113-181 ------------------

@@ -102,6 +102,7 @@ struct acmmp_ctx {
     // every other context's kernels: reallocating per problem serialised the pipeline's contexts)
     size_t dep_cap = 0, scaled_cap = 0, spatial_cap = 0;
     bool has_prior = false;           // set_planar_prior since the last upload_views
+    bool has_result = false;          // planes_rm / costs_rm hold this problem's maps (a run, set_state[_device])
     char* d_pp = nullptr;             // planar-prior triangle tables (acmmp_set_planar_prior_from_maps)
     size_t pp_cap = 0;
     int4* d_support = nullptr;        // support-point blocks (acmmp_set_planar_prior_from_state)
@@ -117,7 +118,7 @@ struct acmmp_ctx {
     float timing[3] = {0.f, 0.f, 0.f};
     std::vector<hipEvent_t> kev;               // 5 per half-sweep (per-kernel timing)
     float ktiming[4] = {0.f, 0.f, 0.f, 0.f};
-    unsigned long long* d_work = nullptr;       // [256] k_eval_nb work counters
+    unsigned long long* d_work = nullptr;       // [256] k_eval_nb work counters + [256] the run's status word
     unsigned long long work_busy = 0, work_total = 0;
     int klaunch[4] = {0, 0, 0, 0};
     int math = ACMMP_MATH_EXACT;                // acmmp_set_math
@@ -457,6 +458,7 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
     // builds a fresh ACMMP object per ProcessProblem, main.cpp:80)
     c->has_prior = false;
     c->has_scaled = false;
+    c->has_result = false;
     c->W = cams[0].width;
     c->H = cams[0].height;
     c->model = cams[0].model;
@@ -714,6 +716,7 @@ acmmp_status acmmp_set_state(acmmp_ctx* c, const float* planes, const float* cos
         HIP_TRY(c, hipMemcpyAsync(c->d_planes_rm, planes, sizeof(float4) * P, hipMemcpyHostToDevice, c->stream));
     if (costs) HIP_TRY(c, hipMemcpyAsync(c->d_costs_rm, costs, sizeof(float) * P, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (planes && costs) c->has_result = true;
     return ACMMP_OK;
 }
 
@@ -739,6 +742,7 @@ acmmp_status acmmp_set_state_device(acmmp_ctx* c, const float* dev_planes, const
         HIP_TRY(c, launch_copy(dev_planes, c->d_planes_rm, sizeof(float4) * P, c->stream));
     if (dev_costs)
         HIP_TRY(c, launch_copy(dev_costs, c->d_costs_rm, sizeof(float) * P, c->stream));
+    if (dev_planes && dev_costs) c->has_result = true;
     // stream-ordered before this context's next kernels; the caller keeps the buffers until its run
     return ACMMP_OK;
 }
@@ -832,6 +836,8 @@ acmmp_status acmmp_set_planar_prior_from_maps(acmmp_ctx* c, const float* depths,
 acmmp_status acmmp_set_planar_prior_from_state(acmmp_ctx* c, float depth_min, float depth_max, int* n_triangles) {
     if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
     if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views and run_patchmatch first");
+    // the maps must be this problem's: a run (or set_state of both maps) since the last upload_views
+    if (!c->has_result) return fail(c, ACMMP_ERR_STATE, "no depth / cost maps since the last upload_views");
     HIP_TRY(c, hipSetDevice(c->device));
     const int W = c->W, H = c->H;
     const size_t nb = static_cast<size_t>((W + 4) / 5) * ((H + 4) / 5);
@@ -974,28 +980,34 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     // b % kNbFixRegions equal) room for every entry its blocks can queue, kNbPix x 8 hypotheses x the
     // launch's views each -- so none is ever dropped (metric 193 MB, C3 656 MB)
     kp.nb_chunk = nb_view_chunk(kp);
-    const bool fixq = c->model == kSphere && c->math == ACMMP_MATH_FAST && c->tex16 && kp.interp &&
-                      Pc < (static_cast<size_t>(1) << 24) && kp.spread_max < 1e30f;
+    // the queue's key holds the colour-grid pixel in 24 bits: a larger grid (views of 8192x4096 and up) has no
+    // queue, and then k_eval_nb does not interpolate (ncc_chunk interpolates only with somewhere to put its
+    // fallbacks).  ACMMP_NBFIX_MAX_PC lowers the limit (a test forces that branch at a small size).
+    size_t fix_max_pc = static_cast<size_t>(1) << 24;
+    if (const char* e = std::getenv("ACMMP_NBFIX_MAX_PC")) fix_max_pc = std::min<size_t>(fix_max_pc, std::strtoull(e, nullptr, 10));
+    const bool fixq = c->model == kSphere && c->math == ACMMP_MATH_FAST && c->tex16 && kp.interp && Pc < fix_max_pc;
+    if (!fixq && c->model == kSphere && c->math == ACMMP_MATH_FAST && c->tex16 && kp.interp && Pc >= fix_max_pc) kp.interp = 0;
     const size_t nb_blocks = (static_cast<size_t>(Pc) + kNbPix - 1) / kNbPix;
     const size_t fix_cap = fixq ? (nb_blocks + kNbFixRegions - 1) / kNbFixRegions * kNbPix * 8 * static_cast<size_t>(kp.nb_chunk) : 0;
     // half-sweep scratch slab: carve the pieces of engine.h's KParams out of one allocation
-    size_t off[17];
+    size_t off[18];
     {
         const size_t VP = static_cast<size_t>(kp.V) * Pc;
-        const size_t sizes[16] = {sizeof(float) * 8 * VP, sizeof(int) * 8 * Pc,
+        const size_t sizes[17] = {sizeof(float) * 8 * VP, sizeof(int) * 8 * Pc,
                                   sizeof(float4) * 5 * Pc, sizeof(float) * 5 * Pc, sizeof(float) * 5 * Pc,
                                   sizeof(PixState) * Pc, sizeof(float) * VP, sizeof(float) * VP,
                                   sizeof(float) * 5 * VP, sizeof(uint32_t) * (5 * Pc + 256),
                                   sizeof(unsigned) * (Pc / 51 + 2),
                                   sizeof(float4) * Pc, sizeof(uint32_t) * kNbFixRegions * fix_cap,
                                   sizeof(unsigned) * kNbFixRegions,
-                                  sizeof(unsigned) * (Pc / 51 + 3), sizeof(uint32_t) * (5 * Pc + 256)};
+                                  sizeof(unsigned) * (Pc / 51 + 3), sizeof(uint32_t) * (5 * Pc + 256),
+                                  sizeof(uint32_t) * 5 * Pc};
         off[0] = 0;
-        for (int k = 0; k < 16; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
+        for (int k = 0; k < 17; ++k) off[k + 1] = (off[k] + sizes[k] + 255) & ~static_cast<size_t>(255);
     }
-    if (c->scratch_bytes < off[16]) {
-        HIP_TRY(c, dalloc(c->d_scratch, off[16]));
-        c->scratch_bytes = off[16];
+    if (c->scratch_bytes < off[17]) {
+        HIP_TRY(c, dalloc(c->d_scratch, off[17]));
+        c->scratch_bytes = off[17];
     }
     kp.cams = c->d_cams;
     kp.tex16 = c->tex16;
@@ -1029,10 +1041,12 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.nbfix_count = reinterpret_cast<unsigned*>(c->d_scratch + off[13]);
     kp.surv_pre = reinterpret_cast<unsigned*>(c->d_scratch + off[14]);
     kp.surv_dense = reinterpret_cast<uint32_t*>(c->d_scratch + off[15]);
+    kp.cand_rough = reinterpret_cast<uint32_t*>(c->d_scratch + off[16]);
     kp.nbfix_cap = static_cast<unsigned>(fix_cap);
     kp.ref_split = ref_split_point(kp.V, Pc, kp.model == kSphere && kp.fast && kp.tex16 && kp.interp && kp.V > 4);
-    if (!c->d_work) HIP_TRY(c, dalloc(c->d_work, 256));
+    if (!c->d_work) HIP_TRY(c, dalloc(c->d_work, 257));
     kp.work = c->d_work;
+    kp.status = reinterpret_cast<unsigned*>(c->d_work + 256);
     kp.nb_views = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     kp.nb_count_work = 1;
     return ACMMP_OK;
@@ -1047,7 +1061,7 @@ acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx* c, uint64_t seed, int n_half_swe
     if (n_half_sweeps < 0) n_half_sweeps = 2 * c->params.max_iterations;
     const size_t Pc = static_cast<size_t>(kp.Pc);
     hipStream_t s = c->stream;
-    HIP_TRY(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long) * 256, s));
+    HIP_TRY(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long) * 257, s));
     HIP_TRY(c, hipEventRecord(c->ev[0], s));
     HIP_TRY(c, launch_init(kp, s));
     // rows outside the reference's checkerboard grid are never rewritten: keep both buffers equal
@@ -1085,8 +1099,10 @@ acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx* c, uint64_t seed, int n_half_swe
     }
     for (int i = 0; i < 3; ++i) HIP_TRY(c, hipEventElapsedTime(&c->timing[i], c->ev[i], c->ev[i + 1]));
     {
-        unsigned long long w[256];
+        unsigned long long w[257];
         HIP_TRY(c, hipMemcpy(w, c->d_work, sizeof w, hipMemcpyDeviceToHost));
+        if (w[256]) return fail(c, ACMMP_ERR_HIP, "run status " + std::to_string(w[256]) + ": an interpolation fallback queue overflowed");
+        c->has_result = true;
         c->work_busy = 0;
         for (int k = 0; k < 256; ++k) c->work_busy += w[k];
         c->work_total = 0;
@@ -1171,7 +1187,7 @@ acmmp_status acmmp_band_begin(acmmp_ctx* c, uint64_t seed, int row0, int row1) {
     kp.filt_lo[1] = kp.row_lo; kp.filt_hi[1] = kp.row_hi;
     const size_t Pc = static_cast<size_t>(kp.Pc);
     hipStream_t s = c->stream;
-    HIP_TRY(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long) * 256, s));
+    HIP_TRY(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long) * 257, s));
     HIP_TRY(c, hipEventRecord(c->ev[0], s));
     HIP_TRY(c, launch_init(kp, s));
     for (int k = 0; k < 2; ++k) {
@@ -1252,6 +1268,10 @@ acmmp_status acmmp_band_end(acmmp_ctx* c, int do_post) {
     }
     for (int i = 0; i < 3; ++i) HIP_TRY(c, hipEventElapsedTime(&c->timing[i], c->ev[i], c->ev[i + 1]));
     c->band_active = false;
+    unsigned long long status = 0;
+    HIP_TRY(c, hipMemcpy(&status, c->d_work + 256, sizeof status, hipMemcpyDeviceToHost));
+    if (status) return fail(c, ACMMP_ERR_HIP, "band run status " + std::to_string(status) + ": an interpolation fallback queue overflowed");
+    c->has_result = true;
     return ACMMP_OK;
 }
 
@@ -1333,7 +1353,8 @@ acmmp_status acmmp_jbu(acmmp_ctx* c, const float* ref, int W, int H, const float
     return ACMMP_OK;
 }
 
-// which: 0 = NCC (per-sample projection), 1 = geom cost, 2 = k_eval_nb's NCC on n pixels x 8 planes
+// which: 0 = NCC (per-sample projection), 1 = geom cost, 2 = k_eval_nb's NCC on n pixels x 8 planes,
+// 3 = the refinement's NCC (k_eval_ref + the tail's fallbacks) on n pixels x 5 planes
 static acmmp_status debug_eval(acmmp_ctx* c, int which, int n, const int* px, const int* py, const float* planes,
                                float* out) {
     if (!c || !px || !py || !planes || !out || n <= 0) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "bad debug args");
@@ -1348,7 +1369,7 @@ static acmmp_status debug_eval(acmmp_ctx* c, int which, int n, const int* px, co
     int *dx = nullptr, *dy = nullptr;
     float4* dp = nullptr;
     float* dout = nullptr;
-    const int per = which == 2 ? 8 : 1;                   // planes per query pixel
+    const int per = which == 2 ? 8 : (which == 3 ? 5 : 1);   // planes per query pixel
     const size_t nout = static_cast<size_t>(n) * per * kp.V;
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&dx), sizeof(int) * n);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&dy), sizeof(int) * n);
@@ -1359,6 +1380,7 @@ static acmmp_status debug_eval(acmmp_ctx* c, int which, int n, const int* px, co
     if (e == hipSuccess) e = hipMemcpy(dp, planes, sizeof(float4) * n * per, hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = which == 2 ? launch_debug_nb(kp, n, dx, dy, dp, dout, c->stream)
+          : which == 3 ? launch_debug_ref(kp, n, dx, dy, dp, dout, c->stream)
                        : launch_debug(kp, which, n, dx, dy, dp, dout, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(float) * nout, hipMemcpyDeviceToHost);
@@ -1375,6 +1397,9 @@ acmmp_status acmmp_debug_geom(acmmp_ctx* c, int n, const int* px, const int* py,
 }
 acmmp_status acmmp_debug_ncc_nb(acmmp_ctx* c, int n, const int* px, const int* py, const float* planes, float* costs) {
     return debug_eval(c, 2, n, px, py, planes, costs);
+}
+acmmp_status acmmp_debug_ncc_ref(acmmp_ctx* c, int n, const int* px, const int* py, const float* planes, float* costs) {
+    return debug_eval(c, 3, n, px, py, planes, costs);
 }
 
 }  // extern "C"

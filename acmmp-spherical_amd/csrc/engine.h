@@ -28,6 +28,7 @@ constexpr int kSphere = 11;
 constexpr int kMaxViews = 32;       // cost_vector[32], uint32 view bitmask (ACMMP.cu:522,1153)
 constexpr int kNbPix = 32;          // k_eval_nb: pixels per 256-lane block (8 lanes each)
 constexpr int kNbFixRegions = 256;  // the queue's regions, one counter each (block % regions)
+constexpr unsigned kStatusFixOverflow = 1u;   // KParams::status: k_nb_fix found a region's queue overfull
 
 struct DevCam {
     // The fields the fast-math sample loop reads come first, contiguous and 16-byte aligned, so each
@@ -147,6 +148,10 @@ struct KParams {
     uint32_t* nbfix;                // kNbFixRegions regions of nbfix_cap entries (every entry a launch can queue)
     unsigned* nbfix_count;          // [kNbFixRegions]
     unsigned nbfix_cap;             // entries per region
+    // k_eval_ref's interpolated instance (SPHERE V > 4): per queued candidate, its selected views of
+    // [0, ref_split) whose interpolation fell back -- k_eval_ref_tail recomputes them and restarts the chain
+    uint32_t* cand_rough;           // [5][Pc]
+    unsigned* status;               // run status bits (kStatus*), zeroed per run, checked after it
 };
 
 // Per-half-sweep output buffers of the colour being updated.
@@ -206,6 +211,9 @@ hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, cons
 // k_eval_nb's NCC instance on n pixels x 8 planes (planes[q * 8 + h]): out[(q * 8 + h) * V + v]
 hipError_t launch_debug_nb(const KParams& kp, int n, const int* px, const int* py, const float4* planes, float* out,
                            hipStream_t s);
+// k_eval_ref's NCC instance (+ the tail's per-sample fallbacks) on n pixels x 5 planes: out[(q * 5 + h) * V + v]
+hipError_t launch_debug_ref(const KParams& kp, int n, const int* px, const int* py, const float4* planes, float* out,
+                            hipStream_t s);
 // Row-pair binary16 copy of one padded view (W + 2) x (H + 2) (DevCam::img16_base layout); *inexact
 // (device int, pre-zeroed) is set when a texel is not exactly representable as a normal binary16
 // number or zero.

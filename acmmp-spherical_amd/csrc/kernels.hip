@@ -663,12 +663,17 @@ __device__ __forceinline__ void sphere_fold_sample(float w, float r, float sp, f
     sss = fmaf(ws, sp, sss);
 }
 
-// fixkey: k_eval_nb's (pixel << 8 | hypothesis << 5) for deferring interpolation fallbacks to k_nb_fix;
-// kFixNone (the default): no fallback -- the refinement kernels' interpolated instances (V > 4), whose
-// inline fallbacks cost C3 6.6 ms per half-sweep (random candidates; profiles/r04_prof_ab.txt) and which
-// the float64 study finds within 1e-4 on every pole / seam / random query tried from 2000x1000 up except
-// pole-straddling patches (k_eval_nb, which takes the most hypotheses, keeps the fallback)
-constexpr uint32_t kFixNone = ~0u;
+// Where the interpolation's nodes spread too far (below) the (pixel, hypothesis, view) must take the per-sample
+// arithmetic instead; the chunk hands those entries on, and interpolates only when it has somewhere to hand
+// them:
+//  * fixkey: k_eval_nb's (pixel << 8 | hypothesis << 5), queued for k_nb_fix, which recomputes them after
+//    the launch;
+//  * kFixNan: the refinement's k_eval_ref (V > 4) gets those costs as NaN (an NCC cost is never NaN: the
+//    clamp of ACMMP.cu:513 maps a NaN ratio to 2.0) and leaves them to k_eval_ref_tail (inline fallbacks there
+//    cost C3 6.6 ms per half-sweep: random candidates, profiles/r04_prof_ab.txt).  (A bitmask handed back
+//    through a pointer instead took k_eval_ref from 120 to 256 VGPRs.)
+// With kFixNone every sample is projected.
+constexpr uint32_t kFixNone = ~0u, kFixNan = ~0u - 1u;
 template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM = 0, bool FULL = false>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv_rt, float (&cost)[VB],
@@ -783,8 +788,9 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     // Views are the outer loop here, and a view's patch columns are taken 0, 2, 3, 5, 1, 4.
     constexpr bool kInterp = FM && MODEL == kSphere && STAGED == 3 && TEX == 1;
     bool interp_done = false;
+    uint32_t rough_nan = 0u;                        // kFixNan: views whose cost becomes NaN
     if constexpr (kInterp) {
-        if (kp.interp) {
+        if (kp.interp && fixkey != kFixNone) {
             interp_done = true;
             // Lagrange weights of patch column / row 1 and 4 on the node columns / rows 0, 2, 3, 5
             constexpr float kL1[4] = {0.26666667f, 1.3333334f, -0.6666667f, 0.06666667f};
@@ -898,8 +904,11 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             // the per-sample fast arithmetic bit for bit -- after the launch.  Done here, one such lane made its
             // whole wave run the 36 projections (3-6% of lanes, so most waves: k_eval_nb +28%).  After the
             // view loop, with no node live (inside it the queue's code spilled).  The queue holds every
-            // entry a launch can produce (capi.cpp sizes it), so none is dropped.
-            if (fixkey != kFixNone) {
+            // entry a launch can produce (capi.cpp sizes it per k_eval_nb launch, and launch_eval_nb runs
+            // k_nb_fix after each), so none is dropped; k_nb_fix flags an overflow, which fails the run.
+            if (fixkey == kFixNan) {
+                rough_nan = rough;
+            } else {
 #pragma unroll
                 for (int v = 0; v < VB; ++v) {
                     if (!has(v)) continue;
@@ -1118,7 +1127,10 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
 #undef ACMMP_ACCUMULATE
 #undef ACMMP_ACCUMULATE_T
 #pragma unroll
-    for (int v = 0; v < VB; ++v) cost[v] = cval[v] ? ncc_cost(sbw[v], srrr[v], ssrs[v], sss[v]) : 2.0f;
+    for (int v = 0; v < VB; ++v) {
+        cost[v] = cval[v] ? ncc_cost(sbw[v], srrr[v], ssrs[v], sss[v]) : 2.0f;
+        if (kInterp && ((rough_nan >> v) & 1u)) cost[v] = __builtin_nanf("");
+    }
 #undef PCV
 }
 
@@ -1259,12 +1271,13 @@ __device__ __forceinline__ void for_all_views(const KParams& kp, int px, int py,
 // texels, exact; 2 = binary16 texels, fast math.
 template <int MODEL, int VB, int STAGED, bool PIPE, int TF, bool PIPE_FM = PIPE, typename F>
 __device__ __forceinline__ void for_all_views_tf(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
-                                                 uint32_t wave_mask, F&& f) {
+                                                 uint32_t wave_mask, F&& f, uint32_t fixkey = kFixNone) {
     if constexpr (TF == 0) {
         if (kp.fast) for_all_views_t<MODEL, VB, STAGED, PIPE_FM, 0, 1>(kp, px, py, pt, ph, wave_mask, f);
         else for_all_views_t<MODEL, VB, STAGED, PIPE, 0, 0>(kp, px, py, pt, ph, wave_mask, f);
     } else {
-        for_all_views_t<MODEL, VB, STAGED, TF == 2 ? PIPE_FM : PIPE, 1, TF == 2 ? 1 : 0>(kp, px, py, pt, ph, wave_mask, f);
+        for_all_views_t<MODEL, VB, STAGED, TF == 2 ? PIPE_FM : PIPE, 1, TF == 2 ? 1 : 0>(kp, px, py, pt, ph, wave_mask, f,
+                                                                                       fixkey);
     }
 }
 static inline int tf_of(const KParams& kp) { return kp.tex16 ? (kp.fast ? 2 : 1) : 0; }
@@ -1895,6 +1908,8 @@ __global__ __launch_bounds__(256) void k_nb_fix(const KParams kp, const int colo
     const int ew = l / kFixLanes, j = l - ew * kFixLanes, e = (t >> 6) * kFixPerWave + ew;
     const unsigned region = blockIdx.x % kNbFixRegions, stripes = gridDim.x / kNbFixRegions;
     const unsigned n = min(kp.nbfix_count[region], kp.nbfix_cap);
+    // sized for every entry a launch can queue (capi.cpp), so this never fires; if it did, the run fails
+    if (t == 0 && blockIdx.x < kNbFixRegions && kp.nbfix_count[region] > kp.nbfix_cap) atomicOr(kp.status, kStatusFixOverflow);
     const uint32_t* q = kp.nbfix + static_cast<long long>(region) * kp.nbfix_cap;
     const long long Pc = kp.Pc;
     for (unsigned i0 = (blockIdx.x / kNbFixRegions) * kFixPerBlock; i0 < n; i0 += stripes * kFixPerBlock) {
@@ -2252,8 +2267,10 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
 }
 
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
+// the interpolated instance (SPHERE V > 4, fast, binary16) is held to 4 waves per SIMD (its geom form took 129
+// VGPRs, 3 waves, once the fallback views are marked)
 template <int MODEL, int VB, bool GEOM, int TF>
-__global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int colour) {
+__global__ __launch_bounds__(256, (MODEL == kSphere && VB > 4 && TF == 2) ? 4 : 1) void k_eval_ref(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
@@ -2298,15 +2315,26 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
     float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
     for (int v = 0; v < kp.V; ++v)
         if (!((amask >> v) & 1u)) vcost[v * Pc] = __builtin_nanf("");
+    // The fast SPHERE V > 4 instance interpolates sample coordinates (ncc_chunk) and gets back the views whose
+    // interpolation nodes spread too far (`rough`): those costs are not taken here -- vcost NaN (not evaluated),
+    // no term in the chain -- and k_eval_ref_tail recomputes them with every sample projected (the per-sample
+    // fast bits).  The chain over the other views is still a lower bound of the final one (below), so the
+    // pruning stays exact; a survivor with rough selected views restarts its chain in the tail.
+    constexpr bool kRefInterp = MODEL == kSphere && kStaged == 3 && TF == 2;
+    uint32_t rough = 0u;
     for_all_views_tf<MODEL, VBA, kStaged, kRefPipe, TF>(kp, px, py, pt, tp, amask, [&](int v, float c) {
         vcost[v * Pc] = c;
+        const bool r = kRefInterp && c != c;
+        if (r) rough |= 1u << v;
         const float w = vw_get(vwp, v);
-        if (w > 0.0f) {
+        if (w > 0.0f && !r) {
             if (GEOM) temp_cost = fmaf(w, fmaf(0.1f, geom_cost<MODEL>(kp, v + 1, tp, px, py, dc), c), temp_cost);
             else temp_cost = fmaf(w, c, temp_cost);
         }
-    });
+    }, kRefInterp ? kFixNan : kFixNone);
     const float partial = temp_cost / weight_norm;
+    // no split: the whole wave sits in the degenerate band (no sample taken, so nothing rough) or the launch has
+    // no tail (launch_eval_ref turns the interpolation off then)
     if (!split) { kp.cand_cost[h * Pc + ci] = partial; return; }
     // Every remaining term w * (c [+ 0.1 geom]) is >= 0 (c in [0, 2], geom in [0, 3]), so the fma chain
     // only grows and, divided by weight_norm > 0, the final cost is >= `partial`: when
@@ -2315,9 +2343,13 @@ __global__ __launch_bounds__(256) void k_eval_ref(const KParams kp, const int co
     // restricted cost instead and always finish.  A survivor that selected no view >= S still goes to
     // the tail: the views >= S its wave evaluates complete its cost vector, which the current-plane
     // cost cache takes over if it wins (a NaN entry there costs k_select a divergent re-evaluation).
+    // With rough views left out the chain skips some non-negative terms; fma is monotone in its addend and
+    // each skipped step never lowers the full chain, so the partial chain still bounds the final cost from
+    // below bit for bit, and the pruning stays exact.
     const PixState& st = kp.pst[ci];
     const bool done = !(st.flags & 1u) && !(partial < st.cost_now);
     kp.cand_cost[h * Pc + ci] = done ? partial : temp_cost;
+    if (kRefInterp && !done) kp.cand_rough[h * Pc + ci] = rough & mask;   // the tail's restart views
     const unsigned long long b = __ballot(!done);
     if (b) {                                                 // queue the wave's survivors in the block's slots
         const int lane = __lane_id();
@@ -2408,7 +2440,13 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
         const uint4 vw = st.vw;
         const float weight_norm = st.weight_norm;
         const uint32_t vwp[4] = {vw.x, vw.y, vw.z, vw.w};
-        uint32_t mask = 0u;
+        // k_eval_ref's interpolated instance (SPHERE V > 4, fast, binary16) left out the selected views of
+        // [0, S) whose interpolation nodes spread too far (`need`): they are evaluated here with every sample
+        // projected, and the candidate's chain restarts from view 0, folding k_eval_ref's stored costs of its
+        // other views in view order -- the chain k_eval_ref would have formed with the per-sample costs there
+        constexpr bool kRefInterp = MODEL == kSphere && VB > 4 && TF == 2;
+        const uint32_t need = kRefInterp ? kp.cand_rough[h * Pc + ci] : 0u;
+        uint32_t mask = need;
         for (int v = S; v < kp.V; ++v) if (vw_get(vwp, v) > 0.0f) mask |= 1u << v;
         const uint32_t umask = wave_or(mask, kp.V);
         const float4 dc = ray_at<MODEL>(kp, px, py);
@@ -2417,8 +2455,20 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
         const float4 ps = kp.psum[ci];
         pt.rw = nullptr; pt.rr = nullptr; pt.wr = nullptr; pt.row = pt.col = nullptr; pt.stride = 0;
         pt.sbw = ps.x; pt.sref = ps.y; pt.srr = ps.z; pt.center = ps.w;
-        float temp_cost = kp.cand_cost[h * Pc + ci];
+        float temp_cost = need ? 0.0f : kp.cand_cost[h * Pc + ci];
         float* vcost = kp.cand_vcost + static_cast<long long>(h) * kp.V * Pc + ci;
+        auto add_term = [&](int v, float c) {
+            const float w = vw_get(vwp, v);
+            if (w > 0.0f) {
+                if (GEOM) temp_cost = fmaf(w, fmaf(0.1f, geom_cost<MODEL>(kp, v + 1, tp, px, py, dc), c), temp_cost);
+                else temp_cost = fmaf(w, c, temp_cost);
+            }
+        };
+        int nxt = need ? 0 : S;                              // restart: next stored view of [0, S) to fold
+        auto fold_stored = [&](int upto) {
+            for (; nxt < upto; ++nxt)
+                if (!((need >> nxt) & 1u)) add_term(nxt, vcost[nxt * Pc]);
+        };
         // SPHERE V > 4: 4-view chunks (87 VGPRs, 5 waves) -- each chunk recomputes the 36 samples' rays,
         // weights and reference texels, so fewer chunks save that work: C3 k_eval_ref + tail 10.52 -> 9.03 ms
         // against 2-view chunks (74 VGPRs, 6 waves), +5.4% (profiles/r04_ab6_ab.txt)
@@ -2431,13 +2481,12 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
         constexpr int VBT = (MODEL == kSphere && VB > 4) ? ACMMP_TAIL_SPH_VB
                           : (MODEL == kPinhole && VB > 4) ? ACMMP_TAIL_PIN_VB : ref_vb<MODEL, VB>();
         for_all_views_tf<MODEL, VBT, 0, kRefPipe, TF>(kp, px, py, pt, tp, umask, [&](int v, float c) {
+            if (kRefInterp && v < S && !((need >> v) & 1u)) return;     // another lane's restart view
+            if (kRefInterp && need) fold_stored(v < S ? v : S);
             vcost[v * Pc] = c;
-            const float w = vw_get(vwp, v);
-            if (w > 0.0f) {
-                if (GEOM) temp_cost = fmaf(w, fmaf(0.1f, geom_cost<MODEL>(kp, v + 1, tp, px, py, dc), c), temp_cost);
-                else temp_cost = fmaf(w, c, temp_cost);
-            }
+            add_term(v, c);
         });
+        if (kRefInterp && need) fold_stored(S);
         kp.cand_cost[h * Pc + ci] = temp_cost / weight_norm;
     }
 }
@@ -2783,20 +2832,21 @@ hipError_t launch_eval_nb(const KParams& kp0, int colour, hipStream_t s) {
     // interpolation fallbacks deferred to k_nb_fix: fast SPHERE with interpolated coordinates only
     const bool fix = kp.nbfix && kp.model == kSphere && kp.fast && kp.tex16 && kp.interp;
     if (!fix) kp.nbfix = nullptr;
-    hipError_t e0 = hipSuccess;
-    if (fix && (e0 = hipMemsetAsync(kp.nbfix_count, 0, sizeof(unsigned) * kNbFixRegions, s)) != hipSuccess) return e0;
     const int chunk = kp.nb_chunk;                          // nb_view_chunk, fixed when the run's KParams were built
     for (int v0 = 0; v0 < kp.V; v0 += chunk) {
         const int v1 = std::min(kp.V, v0 + chunk);
         const uint32_t hi = v1 >= 32 ? 0xFFFFFFFFu : ((1u << v1) - 1u);
         kp.nb_views = hi & ~((1u << v0) - 1u);
         kp.nb_count_work = v0 == 0;
-        const hipError_t e = launch_eval_nb_views(kp, colour, s);
-        if (e != hipSuccess) return e;
-    }
-    if (fix) {
-        k_nb_fix<1><<<16 * kNbFixRegions, 256, 0, s>>>(kp, colour);   // 16 stripes per region
-        return hipGetLastError();
+        // the queue holds one launch's entries (a region's lanes x the chunk's views): emptied before and
+        // drained after every view chunk
+        hipError_t e = hipSuccess;
+        if (fix && (e = hipMemsetAsync(kp.nbfix_count, 0, sizeof(unsigned) * kNbFixRegions, s)) != hipSuccess) return e;
+        if ((e = launch_eval_nb_views(kp, colour, s)) != hipSuccess) return e;
+        if (fix) {
+            k_nb_fix<1><<<16 * kNbFixRegions, 256, 0, s>>>(kp, colour);   // 16 stripes per region
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
     }
     return hipSuccess;
 }
@@ -2861,7 +2911,7 @@ hipError_t launch_debug_nb(const KParams& kp0, int n, const int* px, const int* 
     // the hook takes k_eval_nb's path, deferred fallbacks included
     KParams kp = kp0;
     const bool fix = kp.nbfix && kp.model == kSphere && kp.fast && kp.tex16 && kp.interp && n < (1 << 24);
-    if (!fix) kp.nbfix = nullptr;
+    if (!fix) kp.nbfix = nullptr;                           // (ncc_chunk then projects every sample)
     // the queue holds every entry: a region's blocks x 256 lanes x all V views (one launch here)
     if (fix && static_cast<long long>(cdiv(cdiv(n, kNbPix), kNbFixRegions)) * 256 * kp.V > kp.nbfix_cap)
         return hipErrorInvalidValue;
@@ -2925,7 +2975,10 @@ hipError_t launch_select(const KParams& kp, int colour, int iter, hipStream_t s)
 #endif  // ACMMP_IN_TU(3)
 
 #if ACMMP_IN_TU(4)
-hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s) {
+hipError_t launch_eval_ref(const KParams& kp0, int colour, hipStream_t s) {
+    // the interpolated refinement leaves its rough views to k_eval_ref_tail: none without a split
+    KParams kp = kp0;
+    if (kp.ref_split <= 0) kp.interp = 0;
     const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
     const size_t lds_ref = (kp.model == kSphere && pick_vb(kp.V) <= 4) ? sep_lds_bytes(kp.S, kp.nside, kRefPix)
                                                                        : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
@@ -2944,6 +2997,59 @@ hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s) {
         if (kp.geom) ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, true, TF><<<grd, 256, 0, s>>>(kp, colour, nref))));
         else ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, false, TF><<<grd, 256, 0, s>>>(kp, colour, nref))));
     }
+    return hipGetLastError();
+}
+
+// Test hook (acmmp_debug_ncc_ref): the refinement's NCC on given queries of one pixel and 5 planes (the 5
+// candidates of PlaneHypothesisRefinement, ACMMP.cu:797-936) -- k_eval_ref's staging and NCC instance over
+// all views, and for the views whose interpolation fell back (fast SPHERE, V > 4) the per-sample arithmetic
+// k_eval_ref_tail recomputes them with.  out[(q * 5 + h) * V + v].
+template <int MODEL, int VB, int TF>
+__global__ __launch_bounds__(256) void k_debug_ref(const KParams kp, int n, const int* __restrict__ qx,
+                                                   const int* __restrict__ qy, const float4* __restrict__ planes,
+                                                   float* __restrict__ out) {
+    extern __shared__ float4 lds4[];
+    const int t = threadIdx.x;
+    const int lp = t / kRefLanes, h = t - lp * kRefLanes;
+    const int q = blockIdx.x * kRefPix + lp;
+    const bool valid = t < kRefPix * kRefLanes && q < n;
+    const int px = valid ? qx[q] : 0, py = valid ? qy[q] : 0;
+    constexpr int kStaged = (MODEL == kSphere && VB <= 4) ? 4 : 3;
+    Patch pt;
+    if constexpr (kStaged == 4) pt = coop_patch_sep<kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
+    else pt = coop_patch_nb<MODEL, kRefPix, kRefLanes>(kp, valid, px, py, lp, h, lds4);
+    constexpr int VBA = ref_vb_eval<MODEL, VB, TF>();
+    if (!valid) return;
+    const long long k = static_cast<long long>(q) * kRefLanes + h;
+    const float4 ph = planes[k];
+    float* o = out + k * kp.V;
+    const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
+    constexpr bool kRefInterp = MODEL == kSphere && kStaged == 3 && TF == 2;
+    uint32_t rough = 0u;
+    for_all_views_tf<MODEL, VBA, kStaged, kRefPipe, TF>(kp, px, py, pt, ph, all, [&](int v, float c) {
+        o[v] = c;
+        if (kRefInterp && c != c) rough |= 1u << v;
+    }, kRefInterp ? kFixNan : kFixNone);
+    if (kRefInterp) {
+        const uint32_t um = wave_or(rough, kp.V);
+        if (um) {
+            const Patch pu = make_patch<MODEL>(kp, px, py);
+            constexpr int VBT = (MODEL == kSphere && VB > 4) ? ACMMP_TAIL_SPH_VB : ref_vb<MODEL, VB>();
+            for_all_views_tf<MODEL, VBT, 0, kRefPipe, TF>(kp, px, py, pu, ph, um, [&](int v, float c) {
+                if ((rough >> v) & 1u) o[v] = c;
+            });
+        }
+    }
+}
+
+hipError_t launch_debug_ref(const KParams& kp0, int n, const int* px, const int* py, const float4* planes, float* out,
+                            hipStream_t s) {
+    KParams kp = kp0;
+    if (kp.ref_split <= 0) kp.interp = 0;                   // launch_eval_ref's rule
+    const size_t lds_ref = (kp.model == kSphere && pick_vb(kp.V) <= 4) ? sep_lds_bytes(kp.S, kp.nside, kRefPix)
+                                                                       : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
+    const dim3 grd = static_cast<unsigned>(cdiv(n, kRefPix));
+    ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_debug_ref<M, VBC, TF><<<grd, 256, lds_ref, s>>>(kp, n, px, py, planes, out))));
     return hipGetLastError();
 }
 #endif  // ACMMP_IN_TU(4)

@@ -362,9 +362,18 @@ acmmp_status acmmp_debug_ncc(acmmp_ctx *ctx, int n, const int *px, const int *py
 /* costs[(k*8 + h)*(num_images-1) + v] = ComputeBilateralNCC (ACMMP.cu:405-516) of plane
  * planes[k*8 + h] at pixel (px[k], py[k]) against source v+1, evaluated by k_eval_nb's own NCC
  * code (the propagation kernel of CheckerboardPropagation, ACMMP.cu:1146-1233): in the fast math
- * mode on SPHERE views from 1600x800 up, with its interpolated sample coordinates. */
+ * mode on SPHERE views whose 6x6 patch spans at most 5 pixels of 2 pi / 2000 rad (patch_size 11,
+ * radius_increment 2: from 2000x1000 up; patch_size 21 / increment 4: from 4000x2000 up), with its
+ * interpolated sample coordinates and their deferred per-sample fallbacks. */
 acmmp_status acmmp_debug_ncc_nb(acmmp_ctx *ctx, int n, const int *px, const int *py, const float *planes,
                                 float *costs);
+/* costs[(k*5 + h)*(num_images-1) + v]: the same NCC of plane planes[k*5 + h] at pixel (px[k], py[k]) as
+ * PlaneHypothesisRefinement (ACMMP.cu:797-936) evaluates its 5 candidates -- k_eval_ref's staging and NCC
+ * instance, which in the fast math mode interpolates SPHERE sample coordinates above 4 source views (the
+ * size gate of acmmp_debug_ncc_nb), and for the views whose interpolation falls back the per-sample costs
+ * k_eval_ref_tail recomputes them with. */
+acmmp_status acmmp_debug_ncc_ref(acmmp_ctx *ctx, int n, const int *px, const int *py, const float *planes,
+                                 float *costs);
 /* out[k*(num_images-1) + v] = ComputeGeomConsistencyCost (ACMMP.cu:646-671). */
 acmmp_status acmmp_debug_geom(acmmp_ctx *ctx, int n, const int *px, const int *py, const float *planes,
                               float *out);

@@ -238,3 +238,105 @@ def test_deferred_fallbacks_are_per_sample_bit_exact(ctx, name, monkeypatch):
         # does not equal the per-sample arithmetic everywhere, so the comparison above tested the queue)
         assert np.mean(product.view(np.uint32) != ps.view(np.uint32)) > 0.2, kind
     ctx.set_math("exact")
+
+
+# ---- the refinement's interpolated NCC (k_eval_ref, SPHERE V > 4) ----------------------------------------
+
+REF_CONFIGS = {
+    "c3-3200x1600-v15": (lambda: scene.sphere_scene(3200, 1600, n_src=15, seed=1234, n_waves=12), 2),
+    "sphere-2000x1000-v6": (lambda: scene.sphere_scene(2000, 1000, n_src=6, seed=77, n_waves=16), 3),
+}
+
+
+def refinement_planes(sc, px, py, seed):
+    """5 planes per pixel shaped like PlaneHypothesisRefinement's candidates (ACMMP.cu:813-874): three near the
+    surface (the current plane, its perturbed depth, its perturbed normal) and two random-normal / random-depth
+    ones, which are the candidates whose interpolation nodes spread far (grazing planes, depth sign flips)."""
+    near = ni.near_surface_planes(sc, px, py, 3, seed=seed)
+    far = ni.near_surface_planes(sc, px, py, 2, seed=seed + 1, spread=1.5, depth_jitter=0.4)
+    return np.concatenate([near, far], axis=1)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", list(REF_CONFIGS))
+def test_interpolated_refinement_per_query(ctx, name, monkeypatch):
+    """acmmp_debug_ncc_ref runs k_eval_ref's staging and NCC instance -- which in the fast mode interpolates SPHERE
+    sample coordinates above 4 source views -- and, for the views whose interpolation nodes spread too far, the
+    per-sample costs k_eval_ref_tail recomputes them with (kernels.hip k_eval_ref / k_eval_ref_tail).  Held per
+    query on the pole / seam / random sets against: the per-sample fast hook (bit for bit where every entry falls
+    back, ACMMP_SPREAD_MAX=-1), the exact mode (k_eval_ref's exact instance = the per-sample exact hook bit for
+    bit) and float64 (np_reference.bilateral_ncc; T1's gates of test_gpu_fastmath.check_t1)."""
+    make, n_f64 = REF_CONFIGS[name]
+    sc = make()
+    c0 = sc.cameras[0]
+    p = types.default_params(num_images=len(sc.images), depth_min=float(c0["depth_min"]) * 0.6,
+                             depth_max=float(c0["depth_max"]) * 1.2)
+    H, W = sc.images[0].shape
+    assert ni.interp_enabled(W, H, p) and len(sc.images) - 1 > 4
+    ctx.set_params(p)
+    ctx.upload_views(sc.images, sc.cameras)
+    report = {}
+    for kind, n in KINDS.items():
+        px, py, _ = ni.special_pixels(sc, kind, n, seed=len(kind) + 41)
+        assert len(px) >= n // 2, (kind, len(px))
+        planes = refinement_planes(sc, px, py, seed=len(kind) + 43)
+        flat_x, flat_y = np.repeat(px, 5), np.repeat(py, 5)
+        ctx.set_math("fast")
+        rf = ctx.debug_ncc_ref(px, py, planes)
+        ps_f = ctx.debug_ncc(flat_x, flat_y, planes.reshape(-1, 4)).reshape(rf.shape)
+        monkeypatch.setenv("ACMMP_SPREAD_MAX", "-1")
+        ctx.set_params(p)
+        every = ctx.debug_ncc_ref(px, py, planes)
+        monkeypatch.delenv("ACMMP_SPREAD_MAX")
+        ctx.set_params(p)
+        ctx.set_math("exact")
+        re_ = ctx.debug_ncc_ref(px, py, planes)
+        ps_e = ctx.debug_ncc(flat_x, flat_y, planes.reshape(-1, 4)).reshape(rf.shape)
+        assert not np.isnan(rf).any() and not np.isnan(every).any()
+        # every entry deferred: the per-sample fast NCC bit for bit (the tail's arithmetic)
+        bad = np.nonzero(every.view(np.uint32) != ps_f.view(np.uint32))
+        assert bad[0].size == 0, (kind, bad[0].size)
+        # k_eval_ref's exact instance is the per-sample exact NCC bit for bit (the oracle's arithmetic)
+        np.testing.assert_array_equal(re_.view(np.uint32), ps_e.view(np.uint32))
+        # the interpolated loop ran
+        assert np.mean(rf.view(np.uint32) != ps_f.view(np.uint32)) > 0.2, kind
+        # float64 on the first n_f64 planes (near-surface) and on the two random candidates
+        sel = list(range(n_f64)) + [3, 4]
+        f, e, pf = rf[:, sel], re_[:, sel], ps_f[:, sel]
+        ref = _f64(sc, p, px, py, planes[:, sel], len(sel), False)
+        agree_fe = np.mean((f >= 2.0) == (e >= 2.0))
+        agree_ef = np.mean((e >= 2.0) == (ref >= 2.0))
+        assert agree_fe >= min(agree_ef, 0.999) - 0.002 and agree_fe >= 0.99, (kind, agree_fe, agree_ef)
+        valid = (e < 2.0) & (f < 2.0) & (ref < 2.0)
+        assert valid.sum() >= 30, (kind, int(valid.sum()))
+        df, de, dfe = np.abs(f - ref)[valid], np.abs(e - ref)[valid], np.abs(f - e)[valid]
+        dpf = np.abs(pf - ref)[valid]
+        assert np.mean(dfe <= 1e-4) >= np.mean(de <= 1e-4) - 0.05, (kind, np.mean(dfe <= 1e-4), np.mean(de <= 1e-4))
+        fast_worse, exact_worse = np.mean(df > de + 1e-4), np.mean(de > df + 1e-4)
+        assert fast_worse <= exact_worse + 0.03, (kind, fast_worse, exact_worse)
+        # no systematic loss against the per-sample fast arithmetic either (its own distance to float64)
+        assert np.mean(df <= 1e-4) >= np.mean(dpf <= 1e-4) - 0.03, (kind, np.mean(df <= 1e-4), np.mean(dpf <= 1e-4))
+        v_all = (rf < 2.0) & (ps_f < 2.0)
+        d_ip = np.abs(rf - ps_f)[v_all]
+        agree_ip = float(np.mean((rf >= 2.0) == (ps_f >= 2.0)))
+        assert agree_ip >= 0.99, (kind, agree_ip)
+        report[kind] = {
+            "pixels": int(len(px)), "queries": int(rf.size), "f64_queries": int(f.size),
+            "fell_back_or_equal_frac": float(np.mean(rf.view(np.uint32) == ps_f.view(np.uint32))),
+            "worst_interp_vs_per_sample_dcost": float(d_ip.max()) if d_ip.size else 0.0,
+            "q99_interp_vs_per_sample_dcost": float(np.quantile(d_ip, 0.99)) if d_ip.size else 0.0,
+            "frac_interp_vs_per_sample_le_1e-4": float(np.mean(d_ip <= 1e-4)) if d_ip.size else 1.0,
+            "worst_interp_vs_f64": float(df.max()), "worst_per_sample_fast_vs_f64": float(dpf.max()),
+            "worst_exact_vs_f64": float(de.max()),
+            "frac_interp_within_1e-4_of_f64": float(np.mean(df <= 1e-4)),
+            "frac_per_sample_fast_within_1e-4_of_f64": float(np.mean(dpf <= 1e-4)),
+            "frac_exact_within_1e-4_of_f64": float(np.mean(de <= 1e-4)),
+            "class_agree_interp_vs_per_sample": agree_ip, "class_agree_interp_vs_exact": float(agree_fe),
+            "class_agree_exact_vs_f64": float(agree_ef),
+        }
+    ctx.set_math("exact")
+    out_dir = os.environ.get("ACMMP_TEST_REPORT_DIR")
+    if out_dir:
+        os.makedirs(out_dir, exist_ok=True)
+        with open(os.path.join(out_dir, f"refinement_queries_{name}.json"), "w") as fh:
+            json.dump(report, fh, indent=1)

@@ -55,3 +55,25 @@ def test_planar_prior_from_state_equals_from_maps(ctx, name, math):
     prior2m, masks2m = ctx.download_planar_prior()
     np.testing.assert_array_equal(masks2, masks2m)
     np.testing.assert_array_equal(prior2.view(np.uint32), prior2m.view(np.uint32))
+
+
+def test_planar_prior_from_state_needs_this_problems_maps(ctx):
+    """After upload_views the context's planes / costs belong to the previous problem: set_planar_prior_from_state
+    refuses (ACMMP_ERR_STATE) until a run or set_state of both maps (capi.cpp has_result)."""
+    sc = scene.sphere_scene(200, 100, n_src=2, seed=29)
+    c0 = sc.cameras[0]
+    p = types.default_params(num_images=len(sc.images), depth_min=float(c0["depth_min"]) * 0.6,
+                             depth_max=float(c0["depth_max"]) * 1.2)
+    dmin, dmax = float(p["depth_min"]), float(p["depth_max"])
+    ctx.set_params(p)
+    ctx.upload_views(sc.images, sc.cameras)
+    ctx.run_patchmatch(3)
+    planes, costs = ctx.download()
+    ctx.upload_views(sc.images, sc.cameras)
+    with pytest.raises(capi.AcmmpError):
+        ctx.set_planar_prior_from_state(dmin, dmax)
+    ctx.set_state(planes, costs)
+    ctx.set_planar_prior_from_state(dmin, dmax)
+    ctx.upload_views(sc.images, sc.cameras)
+    ctx.run_patchmatch(3)
+    ctx.set_planar_prior_from_state(dmin, dmax)
