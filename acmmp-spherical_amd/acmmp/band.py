@@ -10,9 +10,13 @@ whole-view run's bit for bit.
 
 `run_local` drives several contexts in one process and copies the halos device to device.  `run_rank` is one
 rank of a multi-GPU run, with the halo exchange as grouped ncclSend / ncclRecv queued on the engine's stream
-(acmmp_comm_band_exchange).  Both use the engine's own halo row ranges (acmmp_band_halo_ranges).
+(acmmp_comm_band_exchange).  `run_rank_host` is the same rank with the halos through host memory and any
+point-to-point transport (`gloo_exchange`: torch.distributed's gloo backend) -- ranks that share a GPU, or have no
+device-to-device path.  All use the engine's own halo row ranges (acmmp_band_halo_ranges).
 """
 from __future__ import annotations
+
+import numpy as np
 
 HALO = 23
 
@@ -65,3 +69,49 @@ def run_rank(ctx, comm, seed: int, height: int, rank: int, world: int):
     ctx.run_patchmatch_band(seed, lo, hi, comm if world > 1 else None,
                             rank - 1 if rank > 0 else -1, rank + 1 if rank < world - 1 else -1)
     return lo, hi
+
+
+def run_rank_host(ctx, seed: int, height: int, rank: int, world: int, exchange, do_post: bool = True):
+    """This rank's band of a view split over `world` ranks, the halo through host buffers: after every half-sweep
+    the updated colour's rows within HALO of the band's edges go to the neighbouring ranks
+    (acmmp_band_get_rows) and theirs come back (acmmp_band_set_rows).  `exchange(sends, recvs)` moves them:
+    sends = [(peer, rows)], recvs = [(peer, n_pixels)] -> the received rows in recvs' order (gloo_exchange).
+    Returns the band (lo, hi) whose rows of ctx's outputs are final."""
+    bands = split_rows(height, world)
+    if len(bands) != world:
+        raise ValueError(f"{height} rows cannot be split into {world} bands of >= {HALO} rows")
+    lo, hi = bands[rank]
+    wh = (ctx.W + 1) // 2
+    ctx.band_begin(seed, lo, hi)
+    while ctx.band_sweeps_left() > 0:
+        colour = ctx.band_sweep()
+        (sua, sub), (rua, rub), (sda, sdb), (rda, rdb) = ctx.band_halo_ranges()
+        sends, recvs, into = [], [], []
+        if rank > 0:
+            sends.append((rank - 1, ctx.band_get_rows(colour, sua, sub)))
+            recvs.append((rank - 1, (rub - rua) * wh))
+            into.append((rua, rub))
+        if rank < world - 1:
+            sends.append((rank + 1, ctx.band_get_rows(colour, sda, sdb)))
+            recvs.append((rank + 1, (rdb - rda) * wh))
+            into.append((rda, rdb))
+        for (a, b), rows in zip(into, exchange(sends, recvs)):
+            ctx.band_set_rows(colour, a, b, rows)
+    ctx.band_end(do_post)
+    return lo, hi
+
+
+def gloo_exchange(sends, recvs):
+    """`run_rank_host`'s transport over torch.distributed point-to-point (the gloo backend: host tensors only)."""
+    import torch
+    import torch.distributed as dist
+    reqs, bufs = [], []
+    for peer, rows in sends:
+        reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(rows).view(np.int32)), peer))
+    for peer, n in recvs:
+        t = torch.empty((n, 6), dtype=torch.int32)
+        bufs.append(t)
+        reqs.append(dist.irecv(t, peer))
+    for r in reqs:
+        r.wait()
+    return [b.numpy().view(np.uint32) for b in bufs]

@@ -35,7 +35,7 @@ EXPORTS = [
     "acmmp_comm_unique_id", "acmmp_comm_create", "acmmp_comm_destroy", "acmmp_comm_broadcast", "acmmp_comm_after",
     "acmmp_comm_allreduce_max", "acmmp_comm_band_exchange", "acmmp_run_patchmatch_band",
     "acmmp_band_begin", "acmmp_band_sweep", "acmmp_band_sweeps_left", "acmmp_band_halo_ranges",
-    "acmmp_band_copy_rows", "acmmp_band_end",
+    "acmmp_band_copy_rows", "acmmp_band_get_rows", "acmmp_band_set_rows", "acmmp_band_end",
     "acmmp_fusion_create", "acmmp_fusion_set_view", "acmmp_fusion_run", "acmmp_fusion_last_error",
     "acmmp_fusion_destroy", "acmmp_image_cache_create", "acmmp_image_cache_destroy", "acmmp_image_cache_stats",
     "acmmp_upload_views_keyed",
@@ -116,6 +116,8 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_band_sweeps_left.argtypes = [vp]
     L.acmmp_band_halo_ranges.argtypes = [vp, vp]
     L.acmmp_band_copy_rows.argtypes = [vp, vp, i32, i32, i32]
+    L.acmmp_band_get_rows.argtypes = [vp, i32, i32, i32, vp, vp, vp]
+    L.acmmp_band_set_rows.argtypes = [vp, i32, i32, i32, vp, vp, vp]
     L.acmmp_band_end.argtypes = [vp, i32]
     L.acmmp_fusion_create.argtypes = [i32, i32, vp, C.POINTER(vp)]
     L.acmmp_fusion_set_view.argtypes = [vp, i32, vp, vp, vp]
@@ -435,6 +437,24 @@ class Context:
 
     def band_copy_rows_from(self, src: "Context", colour: int, row_a: int, row_b: int):
         self._check(self.L.acmmp_band_copy_rows(self.h, src.h, colour, row_a, row_b), "band_copy_rows")
+
+    def band_get_rows(self, colour: int, row_a: int, row_b: int) -> np.ndarray:
+        """Rows [row_a, row_b) of `colour`'s current band state as one host array of 6 words per colour-grid pixel
+        (plane x, y, z, w, cost as float32 bits, selected-view mask) -- the host transport of the halo."""
+        n = (row_b - row_a) * ((self.W + 1) // 2)
+        pl = np.empty((n, 4), np.float32)
+        co = np.empty(n, np.float32)
+        sel = np.empty(n, np.uint32)
+        self._check(self.L.acmmp_band_get_rows(self.h, colour, row_a, row_b, _p(pl), _p(co), _p(sel)), "band_get_rows")
+        return np.concatenate([pl.view(np.uint32), co.view(np.uint32)[:, None], sel[:, None]], axis=1)
+
+    def band_set_rows(self, colour: int, row_a: int, row_b: int, rows: np.ndarray):
+        """Inverse of band_get_rows: write the (n, 6) words into `colour`'s current band state."""
+        rows = np.asarray(rows, np.uint32).reshape(-1, 6)
+        pl = np.ascontiguousarray(rows[:, :4]).view(np.float32)
+        co = np.ascontiguousarray(rows[:, 4]).view(np.float32)
+        sel = np.ascontiguousarray(rows[:, 5])
+        self._check(self.L.acmmp_band_set_rows(self.h, colour, row_a, row_b, _p(pl), _p(co), _p(sel)), "band_set_rows")
 
     def band_end(self, do_post: bool = True):
         self._check(self.L.acmmp_band_end(self.h, int(do_post)), "band_end")

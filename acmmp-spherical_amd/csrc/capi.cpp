@@ -1250,6 +1250,40 @@ acmmp_status acmmp_band_copy_rows(acmmp_ctx* dst, acmmp_ctx* src, int colour, in
     return ACMMP_OK;
 }
 
+acmmp_status acmmp_band_get_rows(acmmp_ctx* c, int colour, int row_a, int row_b, float* planes, float* costs,
+                                 uint32_t* sel) {
+    if (!c || !planes || !costs || !sel) return ACMMP_ERR_INVALID_ARGUMENT;
+    BandBuffers b{};
+    const acmmp_status st = band_buffers(c, colour, &b);
+    if (st != ACMMP_OK) return st;
+    if (row_a < 0 || row_b > c->H || row_a > row_b) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "rows out of range");
+    if (row_a == row_b) return ACMMP_OK;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));            // the half-sweep that wrote them is complete
+    const size_t off = static_cast<size_t>(row_a) * b.Wh, n = static_cast<size_t>(row_b - row_a) * b.Wh;
+    HIP_TRY(c, hipMemcpy(planes, b.plane + off, sizeof(float4) * n, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(costs, b.cost + off, sizeof(float) * n, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(sel, b.sel + off, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_band_set_rows(acmmp_ctx* c, int colour, int row_a, int row_b, const float* planes, const float* costs,
+                                 const uint32_t* sel) {
+    if (!c || !planes || !costs || !sel) return ACMMP_ERR_INVALID_ARGUMENT;
+    BandBuffers b{};
+    const acmmp_status st = band_buffers(c, colour, &b);
+    if (st != ACMMP_OK) return st;
+    if (row_a < 0 || row_b > c->H || row_a > row_b) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "rows out of range");
+    if (row_a == row_b) return ACMMP_OK;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t off = static_cast<size_t>(row_a) * b.Wh, n = static_cast<size_t>(row_b - row_a) * b.Wh;
+    HIP_TRY(c, hipMemcpyAsync(b.plane + off, planes, sizeof(float4) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(b.cost + off, costs, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(b.sel + off, sel, sizeof(uint32_t) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));            // the caller's (pageable) buffers may go next
+    return ACMMP_OK;
+}
+
 acmmp_status acmmp_band_end(acmmp_ctx* c, int do_post) {
     if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
     if (!c->band_active) return fail(c, ACMMP_ERR_STATE, "band_begin first");

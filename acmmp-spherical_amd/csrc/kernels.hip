@@ -627,6 +627,9 @@ __device__ __forceinline__ Patch make_patch(const KParams& kp, int px, int py) {
 // The NCC of one view from its weighted sums (ACMMP.cu:500-516): sbw = sum w, srrr = (sum w r, sum w r r),
 // ssrs = (sum w s, sum w r s), sss = sum w s s
 __device__ __forceinline__ float ncc_cost(float sbw, f32x2 srrr, f32x2 ssrs, float sss) {
+    // sbw and the reference sums through an opaque copy: their reciprocal, mean and variance are the same for
+    // every view and hypothesis, and hoisted to the prologue they were kept (and spilled) across the view loop
+    asm volatile("" : "+v"(sbw), "+v"(srrr));
     float out = 2.0f;
     if (!(sbw < 1e-6f)) {
         const float inv = 1.0f / sbw;
@@ -666,14 +669,25 @@ __device__ __forceinline__ void sphere_fold_sample(float w, float r, float sp, f
 // Where the interpolation's nodes spread too far (below) the (pixel, hypothesis, view) must take the per-sample
 // arithmetic instead; the chunk hands those entries on, and interpolates only when it has somewhere to hand
 // them:
-//  * fixkey: k_eval_nb's (pixel << 8 | hypothesis << 5), queued for k_nb_fix, which recomputes them after
-//    the launch;
+//  * fixkey = the wave's first colour-grid pixel (k_eval_nb's 8-lanes-per-pixel layout: lane l of the wave takes
+//    pixel fixkey + l / 8 and hypothesis l % 8): the entry (pixel << 8 | hypothesis << 5 | view) is queued for
+//    k_nb_fix, which recomputes it after the launch.  The key is formed at the queue from the lane id, so
+//    nothing per lane stays live across the view loop for it (a per-lane key spilled at the 7-wave budget);
 //  * kFixNan: the refinement's k_eval_ref (V > 4) gets those costs as NaN (an NCC cost is never NaN: the
 //    clamp of ACMMP.cu:513 maps a NaN ratio to 2.0) and leaves them to k_eval_ref_tail (inline fallbacks there
 //    cost C3 6.6 ms per half-sweep: random candidates, profiles/r04_prof_ab.txt).  (A bitmask handed back
 //    through a pointer instead took k_eval_ref from 120 to 256 VGPRs.)
 // With kFixNone every sample is projected.
 constexpr uint32_t kFixNone = ~0u, kFixNan = ~0u - 1u;
+
+// The lane's index in its wave, read where it is used: an asm volatile statement is neither hoisted nor merged
+// with another read, so a value derived from it is not kept live from the prologue (k_eval_nb spilled its lane
+// id, output pointer and queue key at the 7-wave budget: 4 of its 5 spilled dwords).
+__device__ __forceinline__ int lane_id_here() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM = 0, bool FULL = false>
 __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                           const int (&vlist)[VB], int nv_rt, float (&cost)[VB],
@@ -787,11 +801,12 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     // tests/test_gpu_fastmath.py hold unchanged (k_eval_nb 1.75 -> 1.51 ms, profiles/r03_interp_ab.txt).
     // Views are the outer loop here, and a view's patch columns are taken 0, 2, 3, 5, 1, 4.
     constexpr bool kInterp = FM && MODEL == kSphere && STAGED == 3 && TEX == 1;
-    bool interp_done = false;
+    int interp_done = 0;                            // (an int: a bool phi became a 0/1 VGPR)
     uint32_t rough_nan = 0u;                        // kFixNan: views whose cost becomes NaN
     if constexpr (kInterp) {
-        if (kp.interp && fixkey != kFixNone) {
-            interp_done = true;
+        // two uniform branches: the condition as one i1 was kept as a 0/1 VGPR across the view loop (spilled)
+        if (kp.interp) if (fixkey != kFixNone) {
+            interp_done = 1;
             // Lagrange weights of patch column / row 1 and 4 on the node columns / rows 0, 2, 3, 5
             constexpr float kL1[4] = {0.26666667f, 1.3333334f, -0.6666667f, 0.06666667f};
             constexpr float kL4[4] = {0.06666667f, -0.6666667f, 1.3333334f, 0.26666667f};
@@ -838,14 +853,31 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         sss[v] = fmaf(ws, sp, sss[v]);
                     }
                 };
-                // the view's 16 nodes first -- independent projections the scheduler interleaves (r03 A/B
-                // against projecting each node column just before its samples: k_eval_nb -1%, 2 VGPRs spilled
-                // instead of 4, profiles/r03_interp_form_ab.txt) -- with x as offsets from the first node,
-                // unwrapped across the seam: small numbers, so the interpolation's rounding stays far below
-                // the positions' own
-                f32x2 nd[4][4];                             // (x - x00 unwrapped, y) per node
+                // Node column by node column (patch columns 0, 2, 3, 5): its 4 nodes projected, its samples taken,
+                // its share of the interpolated columns 1 and 4 at the node rows accumulated -- so one node column
+                // (8 VGPRs) and the two interpolated columns (16) are live instead of all 16 nodes (32; the whole
+                // view's nodes first spilled at the 7-wave budget once the view loop's other values grew).  x is
+                // the offset from the first node, unwrapped across the seam: small numbers, so the interpolation's
+                // rounding stays far below the positions' own.  The same values in the same sample order as
+                // projecting all nodes first (round 3's form), so the same bits.
+                f32x2 c1[4], c4[4];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) c1[b] = c4[b] = splat2(0.f);
+                // The interpolation holds where the source mapping is smooth over the patch.  Where the four
+                // corner nodes spread over more than kp.spread_max (256) source pixels in x or y -- a patch
+                // landing next to a source pole (longitude stretches as 1 / cos(latitude)) or a near-grazing
+                // plane whose depth flips sign inside the patch -- the (pixel, hypothesis, view) goes to
+                // k_nb_fix, which projects all 36 samples in the per-sample loop's order and arithmetic (so
+                // those costs are the per-sample fast ones bit for bit).  float64 study (tests/np_interp.py,
+                // tests/test_interp_design.py): with the test, the interpolated NCC stays within 1e-4 of the
+                // projected one on every query tried from 2000x1000 up (capi.cpp's size gate), pole-adjacent
+                // and random planes included; without it the tail reached 0.6.  Corner terms of node column 0
+                // are kept until column 3's (x03, and the y pair's max / min in the same grouping).
+                float x03 = 0.f, y0max = 0.f, y0min = 0.f;
+                bool smooth = true;
 #pragma unroll
                 for (int a = 0; a < 4; ++a) {
+                    f32x2 nd[4];                            // (x - x00 unwrapped, y) per node of this column
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
                         const float4 q = pt.rw[(kNode[a] * 6 + kNode[b]) * pt.stride];
@@ -855,57 +887,47 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         project_fast<MODEL>(c, make_float3(rw.x * dep, rw.y * dep, rw.z * dep), x, y);
                         if (a == 0 && b == 0) {
                             x00 = x;
-                            nd[a][b].x = 0.0f;
+                            nd[b].x = 0.0f;
                         } else {
                             const float dx = x - x00;
-                            nd[a][b].x = fmaf(-rintf(dx * c.invW), c.Wf, dx);
+                            nd[b].x = fmaf(-rintf(dx * c.invW), c.Wf, dx);
                         }
-                        nd[a][b].y = y;
+                        nd[b].y = y;
                     }
-                }
-                // The interpolation holds where the source mapping is smooth over the patch.  Where the four
-                // corner nodes spread over more than kp.spread_max (256) source pixels in x or y -- a patch
-                // landing next to a source pole (longitude stretches as 1 / cos(latitude)) or a near-grazing
-                // plane whose depth flips sign inside the patch -- the (pixel, hypothesis, view) goes to
-                // k_nb_fix, which projects all 36 samples in the per-sample loop's order and arithmetic (so
-                // those costs are the per-sample fast ones bit for bit).  float64 study (tests/np_interp.py,
-                // tests/test_interp_design.py): with the test, the interpolated NCC stays within 1e-4 of the
-                // projected one on every query tried from 2000x1000 up (capi.cpp's size gate), pole-adjacent
-                // and random planes included; without it the tail reached 0.6.
-                const float sx_ = fmaxf(fmaxf(nd[0][3].x, nd[3][0].x), fmaxf(nd[3][3].x, 0.0f)) -
-                                  fminf(fminf(nd[0][3].x, nd[3][0].x), fminf(nd[3][3].x, 0.0f));
-                const float sy_ = fmaxf(fmaxf(nd[0][0].y, nd[0][3].y), fmaxf(nd[3][0].y, nd[3][3].y)) -
-                                  fminf(fminf(nd[0][0].y, nd[0][3].y), fminf(nd[3][0].y, nd[3][3].y));
-                const bool smooth = fmaxf(sx_, sy_) <= spread_max;
-                rough |= smooth ? 0u : (1u << v);
-                // the samples re-read (w, r) from LDS rather than keep the nodes' reads live across the
-                // projections (merged, they spilled 210 VGPRs)
-                asm volatile("" ::: "memory");
-#pragma unroll
-                for (int a = 0; a < 4; ++a) column(kNode[a], nd[a]);
-                // the interpolated columns 1 and 4 at the node rows, formed after the node columns (fewer
-                // values live across them)
-                f32x2 c1[4], c4[4];
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    c1[b] = c4[b] = splat2(0.f);
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) {
-                        c1[b] = pk_fma(splat2(kL1[a]), nd[a][b], c1[b]);
-                        c4[b] = pk_fma(splat2(kL4[a]), nd[a][b], c4[b]);
+                    if (a == 0) {
+                        x03 = nd[3].x;
+                        y0max = fmaxf(nd[0].y, nd[3].y);
+                        y0min = fminf(nd[0].y, nd[3].y);
                     }
+                    if (a == 3) {
+                        const float sx_ = fmaxf(fmaxf(x03, nd[0].x), fmaxf(nd[3].x, 0.0f)) -
+                                          fminf(fminf(x03, nd[0].x), fminf(nd[3].x, 0.0f));
+                        const float sy_ = fmaxf(y0max, fmaxf(nd[0].y, nd[3].y)) - fminf(y0min, fminf(nd[0].y, nd[3].y));
+                        smooth = fmaxf(sx_, sy_) <= spread_max;
+                    }
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        c1[b] = pk_fma(splat2(kL1[a]), nd[b], c1[b]);
+                        c4[b] = pk_fma(splat2(kL4[a]), nd[b], c4[b]);
+                    }
+                    // the samples re-read (w, r) from LDS rather than keep the nodes' reads live across the
+                    // projections (merged, they spilled 210 VGPRs)
+                    column(kNode[a], nd);
+                    __builtin_amdgcn_sched_barrier(0);       // one node column live at a time
                 }
                 column(1, c1);
                 column(4, c4);
+                rough |= smooth ? 0u : (1u << v);
                 __builtin_amdgcn_sched_barrier(0);           // one view's nodes live at a time
             }
             // Lanes whose corners spread too far go to k_nb_fix's queue (fixkey set: k_eval_nb and its test
             // hook), which recomputes those (pixel, hypothesis, view) costs with every sample projected --
             // the per-sample fast arithmetic bit for bit -- after the launch.  Done here, one such lane made its
             // whole wave run the 36 projections (3-6% of lanes, so most waves: k_eval_nb +28%).  After the
-            // view loop, with no node live (inside it the queue's code spilled).  The queue holds every
-            // entry a launch can produce (capi.cpp sizes it per k_eval_nb launch, and launch_eval_nb runs
-            // k_nb_fix after each), so none is dropped; k_nb_fix flags an overflow, which fails the run.
+            // view loop (inside it the queue's code spilled, both before and after the node-column form).
+            // The queue holds every entry a launch can produce (capi.cpp sizes it per k_eval_nb launch, and
+            // launch_eval_nb runs k_nb_fix after each), so none is dropped; k_nb_fix flags an overflow, which
+            // fails the run.  k_eval_ref (kFixNan) gets those costs as NaN instead.
             if (fixkey == kFixNan) {
                 rough_nan = rough;
             } else {
@@ -915,17 +937,18 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                     const bool redo = (rough >> v) & 1u;
                     const unsigned long long b = __ballot(redo);
                     if (b) {
-                        const int lane = __lane_id();
+                        const int lane = lane_id_here();
                         const int leader = __ffsll(static_cast<long long>(b)) - 1;
                         unsigned base = 0u;
                         // one of kNbFixRegions counters per block (a single one serialised the atomics:
                         // k_eval_nb +0.35 ms at the metric)
                         const unsigned region = blockIdx.x % kNbFixRegions;
                         if (lane == leader) base = atomicAdd(kp.nbfix_count + region, static_cast<unsigned>(__popcll(b)));
-                        base = __shfl(base, leader);
+                        base = __builtin_amdgcn_readlane(base, leader);      // (__shfl needs a lane id of its own)
                         const unsigned slot = base + static_cast<unsigned>(__popcll(b & ((1ull << lane) - 1ull)));
-                        if (redo && slot < kp.nbfix_cap)
-                            kp.nbfix[static_cast<long long>(region) * kp.nbfix_cap + slot] = fixkey | static_cast<uint32_t>(cv[v] - 1);
+                        const uint32_t key = ((fixkey + static_cast<uint32_t>(lane >> 3)) << 8) |
+                                             (static_cast<uint32_t>(lane & 7) << 5) | static_cast<uint32_t>(cv[v] - 1);
+                        if (redo && slot < kp.nbfix_cap) kp.nbfix[static_cast<long long>(region) * kp.nbfix_cap + slot] = key;
                     }
                 }
             }
@@ -947,7 +970,7 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     // than the per-sample form's (q99 8e-5 vs 1.7e-4 px).
     constexpr bool kHomog = FM && MODEL == kPinhole && STAGED == 3;
     if constexpr (kHomog) if (kp.homog) {
-        interp_done = true;
+        interp_done = 1;
         ConstCam& c0 = ccams[0];
         const float v0x = (static_cast<float>(px) - c0.K[2]) * c0.inv_fx;
         const float v0y = (static_cast<float>(py) - c0.K[5]) * c0.inv_fy;
@@ -1850,10 +1873,15 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_SPH_WAVES : 
     if (pos < 0) return;
     const float4 ph = plane_at(kp, pos);
     const uint32_t all = kp.nb_views;
-    float* out = kp.hyp_cost + static_cast<long long>(h) * kp.V * Pc + ci;
-    const uint32_t fixkey = kp.nbfix ? (static_cast<uint32_t>(ci) << 8) | (static_cast<uint32_t>(h) << 5) : kFixNone;
+    // the wave's first pixel ci = row_lo * Wh + q (colour_pixel): lane l holds pixel base + l / 8, hypothesis l % 8.
+    // The output address and the fallback key are formed from it and the lane id where they are used.
+    const uint32_t wbase = static_cast<uint32_t>(uniform_int(static_cast<int>(kp.row_lo * kp.Wh + blockIdx.x * kNbPix + (t >> 6) * 8)));
+    const uint32_t fixkey = kp.nbfix ? wbase : kFixNone;
     for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
-        kp, px, py, pt, ph, all, [&](int v, float c) { out[v * Pc] = c; }, fixkey);
+        kp, px, py, pt, ph, all, [&](int v, float c) {
+            const int l = lane_id_here();
+            kp.hyp_cost[(static_cast<long long>(l & 7) * kp.V + v) * Pc + (wbase + (l >> 3))] = c;
+        }, fixkey);
 }
 
 // The interpolation fallbacks k_eval_nb queued (ncc_chunk): each (pixel, hypothesis, view) cost with every
@@ -2269,8 +2297,11 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
 // Aggregated cost of each valid refinement candidate (ACMMP.cu:876-906).
 // the interpolated instance (SPHERE V > 4, fast, binary16) is held to 4 waves per SIMD (its geom form took 129
 // VGPRs, 3 waves, once the fallback views are marked)
+#ifndef ACMMP_REF_INTERP_WAVES
+#define ACMMP_REF_INTERP_WAVES 4
+#endif
 template <int MODEL, int VB, bool GEOM, int TF>
-__global__ __launch_bounds__(256, (MODEL == kSphere && VB > 4 && TF == 2) ? 4 : 1) void k_eval_ref(const KParams kp, const int colour) {
+__global__ __launch_bounds__(256, (MODEL == kSphere && VB > 4 && TF == 2) ? ACMMP_REF_INTERP_WAVES : 1) void k_eval_ref(const KParams kp, const int colour) {
     extern __shared__ float4 lds4[];
     const int t = threadIdx.x;
     const int lp = t / kRefLanes, h = t - lp * kRefLanes;
@@ -2872,7 +2903,7 @@ __global__ __launch_bounds__(256) void k_debug_nb(const KParams kp, int n, const
     const float4 ph = planes[k];
     float* o = out + k * kp.V;
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
-    const uint32_t fixkey = kp.nbfix ? (static_cast<uint32_t>(q) << 8) | (static_cast<uint32_t>(h) << 5) : kFixNone;
+    const uint32_t fixkey = kp.nbfix ? static_cast<uint32_t>(uniform_int(static_cast<int>(blockIdx.x * kNbPix + (t >> 6) * 8))) : kFixNone;
     for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
         kp, px, py, pt, ph, all, [&](int v, float c) { o[v] = c; }, fixkey);
 }

@@ -6,8 +6,9 @@
 // runs it on the host too); compiled with -ffp-contract=off, float/double exactly where the
 // reference's C++ promotes.
 //
-// Delaunay: incremental Bowyer-Watson on the integer support points with exact predicates
-// (64-bit orientation, 128-bit in-circle).  cv::Subdiv2D's triangle order and its choice among
+// Delaunay: divide and conquer (Guibas-Stolfi merges, Dwyer's strips; parallel over host threads) on
+// the integer support points with exact predicates (64-bit orientation, 64/128-bit in-circle); an
+// incremental Bowyer-Watson form is its fallback.  cv::Subdiv2D's triangle order and its choice among
 // co-circular configurations are not reproduced -- that part is "parity unpinned" (SURVEY.md §8c):
 // the device side is pinned by injecting prior planes + masks (acmmp_set_planar_prior).
 #include <algorithm>
@@ -252,6 +253,327 @@ private:
     int last_ = 0;
 };
 
+// Divide-and-conquer Delaunay (Guibas & Stolfi 1985, quad-edge subdivision) in Dwyer's form (1987): the points,
+// sorted by x, are cut into vertical strips of about 2 sqrt(n) points; each strip is triangulated by the same
+// divide and conquer with horizontal cuts (its points sorted by (y, -x): the frame turned by 90 degrees, which
+// the orientation and in-circle predicates do not see), then the strips are merged along vertical seams.  Every
+// merge walks only its seam (with vertical cuts alone the slabs are as tall as the image and each of the log n
+// levels re-walks all of it: 39 ms for 38k points, slower than the incremental form).  Strips triangulate on up
+// to 16 host threads, the top merges too.  Exact predicates as above (64-bit for coordinate differences below
+// 2^14, 128-bit otherwise).  Co-circular points: any triangulation the merges settle on is Delaunay; it need not
+// be the incremental one's (neither is cv::Subdiv2D's), and it does not depend on the thread
+// count (the strips and split points are fixed by n).  The Hilbert-order incremental insertion stays the
+// fallback (duplicate points, fewer than 3 points per strip, edge-pool overflow).
+class DelaunayDC {
+public:
+    explicit DelaunayDC(const std::vector<Pt>& pts) : p_(pts), n_(static_cast<int>(pts.size())) {}
+
+    // false: the incremental form must do it (duplicate points, degenerate strips, edge pool exhausted)
+    bool run() {
+        if (n_ < 3) return false;
+        // (x, y) order: a counting sort on x keeps the input order within one x, which is y order for the
+        // support points (strip-major, rows rising within a strip); anything else gets a comparison sort
+        order_.resize(n_);
+        long long xmin = p_[0].x, xmax = p_[0].x;
+        for (const Pt& q : p_) { xmin = std::min(xmin, q.x); xmax = std::max(xmax, q.x); }
+        auto xy_less = [&](int a, int b) { return p_[a].x != p_[b].x ? p_[a].x < p_[b].x : p_[a].y < p_[b].y; };
+        if (xmax - xmin < 4 * static_cast<long long>(n_) + 65536) {
+            std::vector<int> cnt(static_cast<size_t>(xmax - xmin) + 2, 0);
+            for (const Pt& q : p_) ++cnt[q.x - xmin + 1];
+            for (size_t k = 1; k < cnt.size(); ++k) cnt[k] += cnt[k - 1];
+            for (int i = 0; i < n_; ++i) order_[cnt[p_[i].x - xmin]++] = i;
+            bool sorted = true;
+            for (int i = 1; i < n_ && sorted; ++i) sorted = !xy_less(order_[i], order_[i - 1]);
+            if (!sorted) std::sort(order_.begin(), order_.end(), xy_less);
+        } else {
+            for (int i = 0; i < n_; ++i) order_[i] = i;
+            std::sort(order_.begin(), order_.end(), xy_less);
+        }
+        for (int i = 1; i < n_; ++i)
+            if (p_[order_[i]].x == p_[order_[i - 1]].x && p_[order_[i]].y == p_[order_[i - 1]].y) return false;
+        // strips: a power of two, ~2 sqrt(n) points each, at least 8
+        int S = 1;
+        while (S * 2 <= static_cast<int>(std::sqrt(static_cast<double>(n_)) / 2.0) && n_ / (S * 2) >= 8) S *= 2;
+        strip_lo_.resize(S + 1);
+        for (int k = 0; k <= S; ++k) strip_lo_[k] = static_cast<int>(static_cast<long long>(n_) * k / S);
+        strips_.assign(S, EdgePair{-1, -1});
+        const unsigned hw = std::thread::hardware_concurrency();
+        int T = (S > 1 && n_ >= 4096) ? static_cast<int>(std::min<unsigned>(std::min<unsigned>(hw ? hw : 1, 16u), S)) : 1;
+        if (const char* e = std::getenv("ACMMP_DELAUNAY_THREADS")) T = std::max(1, std::min(T, std::atoi(e)));   // tests
+        // quad pool: each strip thread a contiguous range (a strip of m points never holds more than 3m live
+        // edges -- a planar subdivision -- and reuses its deleted ones), the merges the rest through one counter.
+        // (One shared counter for everything interleaved the threads' quads: false sharing and a contended
+        // atomic made the strips 10x slower.)
+        size_t base = 0;
+        for (int t = 0; t < T; ++t) {
+            pool_[t].bump = base;
+            for (int k = t; k < S; k += T) base += 3 * static_cast<size_t>(strip_lo_[k + 1] - strip_lo_[k]) + 16;
+            pool_[t].end = base;
+            base = (base + 15) & ~static_cast<size_t>(15);     // next thread's range on its own cache lines
+        }
+        merge_base_ = base;
+        next_.store(base);
+        cap_ = base + 3 * static_cast<size_t>(n_) + 1024;
+        onext_.resize(4 * cap_);
+        org_.resize(2 * cap_);
+        alive_.assign(cap_, 0);
+        auto strip_task = [&](int t) {
+            for (int k = t; k < S; k += T) {
+                const int lo = strip_lo_[k], hi = strip_lo_[k + 1];
+                std::sort(order_.begin() + lo, order_.begin() + hi, [&](int a, int b) {
+                    return p_[a].y != p_[b].y ? p_[a].y < p_[b].y : p_[a].x > p_[b].x;
+                });
+                const EdgePair r = build(lo, hi, t);            // (y, -x) frame: edges out of its lowest / highest point
+                strips_[k] = r.le < 0 ? EdgePair{-1, -1} : to_x_frame(r.le);
+            }
+        };
+        {
+            std::vector<std::thread> th;
+            for (int t = 1; t < T; ++t) th.emplace_back(strip_task, t);
+            strip_task(0);
+            for (auto& x : th) x.join();
+        }
+        for (TaskPool& tp : pool_) tp.bump = tp.end = 0;        // the merges allocate through next_
+        for (const EdgePair& e : strips_)
+            if (e.le < 0) return false;
+        // merge the strips along vertical seams; the halves of the top levels on their own threads
+        par_levels_ = 0;
+        for (int t = T; t > 1 && (S >> par_levels_) > 1; t >>= 1) ++par_levels_;
+        for (TaskPool& tp : pool_) tp.free.clear();
+        const EdgePair r = merge_strips(0, S, 0, 0);
+        return r.le >= 0 && !overflow_.load();
+    }
+
+    std::vector<std::array<int, 3>> triangles() const {
+        // every face bounded by three edges and turning left: one triangle, kept from the directed edge leaving
+        // its lowest point index; the quads scanned in parallel ranges
+        std::vector<int> start(static_cast<size_t>(n_) + 1, 0);
+        const size_t used = std::min(next_.load(), cap_);      // (the strip ranges lie below merge_base_)
+        const unsigned hw = std::thread::hardware_concurrency();
+        const int T = used > 65536 ? static_cast<int>(std::min<unsigned>(hw ? hw : 1, 16u)) : 1;
+        std::vector<std::vector<std::array<int, 3>>> part(T);
+        auto scan = [&](int t) {
+            std::vector<std::array<int, 3>>& out = part[t];
+            out.reserve(used / T + 16);
+            for (size_t q = used * t / T; q < used * (t + 1) / T; ++q) {
+                if (!alive_[q]) continue;
+                for (int r = 0; r < 4; r += 2) {
+                    const int e = static_cast<int>(4 * q + r);
+                    const int a = org(e), e1 = lnext(e), b = org(e1);
+                    if (!(a < b)) continue;
+                    const int e2 = lnext(e1), c = org(e2);
+                    if (!(a < c) || lnext(e2) != e) continue;
+                    if (orient(p_[a], p_[b], p_[c]) <= 0) continue;
+                    out.push_back({a, b, c});
+                }
+            }
+        };
+        {
+            std::vector<std::thread> th;
+            for (int t = 1; t < T; ++t) th.emplace_back(scan, t);
+            scan(0);
+            for (auto& x : th) x.join();
+        }
+        std::vector<std::array<int, 3>> tris;
+        for (auto& v : part) tris.insert(tris.end(), v.begin(), v.end());
+        for (const auto& t : tris) ++start[t[0] + 1];
+        for (int i = 0; i < n_; ++i) start[i + 1] += start[i];
+        std::vector<std::array<int, 3>> out(tris.size());
+        std::vector<int> fill(start.begin(), start.end() - 1);
+        for (const auto& t : tris) out[fill[t[0]]++] = t;
+        for (int i = 0; i < n_; ++i)
+            if (start[i + 1] - start[i] > 1) std::sort(out.begin() + start[i], out.begin() + start[i + 1]);
+        return out;
+    }
+
+private:
+    struct EdgePair { int le, re; };
+    // quad-edge navigation: edge e = 4 q + r, r the rotation
+    static int rot(int e) { return (e & ~3) | ((e + 1) & 3); }
+    static int sym(int e) { return (e & ~3) | ((e + 2) & 3); }
+    static int rotinv(int e) { return (e & ~3) | ((e + 3) & 3); }
+    int onext(int e) const { return onext_[e]; }
+    int oprev(int e) const { return rot(onext_[rot(e)]); }
+    int lnext(int e) const { return rot(onext_[rotinv(e)]); }
+    int rprev(int e) const { return onext_[sym(e)]; }
+    int org(int e) const { return org_[(e >> 2) * 2 + ((e & 3) >> 1)]; }
+    int dest(int e) const { return org(sym(e)); }
+    void set_org(int e, int v) { org_[(e >> 2) * 2 + ((e & 3) >> 1)] = v; }
+
+    // -1 when the pool is exhausted (a planar subdivision of n points has < 3n edges, so 6n + 1024 quads hold
+    // every task's live edges and free lists; the check keeps a bad input from writing out of bounds)
+    int make_edge(int tid, int a, int b) {
+        int q;
+        std::vector<int>& fr = pool_[tid].free;
+        if (!fr.empty()) { q = fr.back(); fr.pop_back(); }
+        else if (pool_[tid].bump < pool_[tid].end) { q = static_cast<int>(pool_[tid].bump++); }
+        else {
+            const size_t k = next_.fetch_add(1);
+            if (k >= cap_) { overflow_.store(true); return -1; }
+            q = static_cast<int>(k);
+        }
+        const int e = 4 * q;
+        onext_[e] = e; onext_[e + 2] = e + 2; onext_[e + 1] = e + 3; onext_[e + 3] = e + 1;
+        set_org(e, a); set_org(e + 2, b);
+        alive_[q] = 1;
+        return e;
+    }
+    void splice(int a, int b) {
+        const int al = rot(onext_[a]), be = rot(onext_[b]);
+        std::swap(onext_[a], onext_[b]);
+        std::swap(onext_[al], onext_[be]);
+    }
+    int connect(int tid, int a, int b) {
+        const int e = make_edge(tid, dest(a), org(b));
+        if (e < 0) return e;
+        splice(e, lnext(a));
+        splice(sym(e), b);
+        return e;
+    }
+    void remove(int tid, int e) {
+        splice(e, oprev(e));
+        splice(sym(e), oprev(sym(e)));
+        alive_[e >> 2] = 0;
+        pool_[tid].free.push_back(e >> 2);
+    }
+    bool ccw(int a, int b, int c) const { return orient(p_[a], p_[b], p_[c]) > 0; }
+    bool rightof(int x, int e) const { return ccw(x, dest(e), org(e)); }
+    bool leftof(int x, int e) const { return ccw(x, org(e), dest(e)); }
+    bool in_circle(int a, int b, int c, int d) const { return incircle(p_[a], p_[b], p_[c], p_[d]) > 0; }
+    bool xless(int a, int b) const { return p_[a].x != p_[b].x ? p_[a].x < p_[b].x : p_[a].y < p_[b].y; }
+
+    // A strip triangulated in the (y, -x) frame hands back the hull edge out of its first point with the outer
+    // face on its right; walking the hull (sym . lnext . sym steps to the previous such edge) finds the (x, y)
+    // frame's pair: the one out of the leftmost point, and the reverse of the one into the rightmost.
+    EdgePair to_x_frame(int e0) const {
+        int e = e0, le = -1, into_r = -1, vl = org(e0), vr = org(e0);
+        size_t guard = 0;
+        do {
+            if (xless(org(e), vl) || org(e) == vl) { vl = org(e); le = e; }
+            if (!xless(dest(e), vr)) { vr = dest(e); into_r = e; }
+            e = sym(lnext(sym(e)));
+        } while (e != e0 && ++guard < 4 * static_cast<size_t>(n_) + 16);
+        if (le < 0 || into_r < 0) return {-1, -1};
+        return {le, sym(into_r)};
+    }
+
+    // the Delaunay triangulation of order_[lo, hi) (sorted in the frame it is cut in): (le, re) = the
+    // counter-clockwise hull edge out of its first point and the clockwise hull edge out of its last
+    EdgePair build(int lo, int hi, int tid) {
+        const int n = hi - lo;
+        if (overflow_.load(std::memory_order_relaxed)) return {-1, -1};
+        if (n == 2) {
+            const int a = make_edge(tid, order_[lo], order_[lo + 1]);
+            if (a < 0) return {-1, -1};
+            return {a, sym(a)};
+        }
+        if (n == 3) {
+            const int s1 = order_[lo], s2 = order_[lo + 1], s3 = order_[lo + 2];
+            const int a = make_edge(tid, s1, s2);
+            const int b = a < 0 ? -1 : make_edge(tid, s2, s3);
+            if (b < 0) return {-1, -1};
+            splice(sym(a), b);
+            if (ccw(s1, s2, s3)) { if (connect(tid, b, a) < 0) return {-1, -1}; return {a, sym(b)}; }
+            if (ccw(s1, s3, s2)) { const int c = connect(tid, b, a); if (c < 0) return {-1, -1}; return {sym(c), c}; }
+            return {a, sym(b)};                              // collinear
+        }
+        const int mid = lo + n / 2;
+        const EdgePair L = build(lo, mid, tid);
+        const EdgePair R = build(mid, hi, tid);
+        return merge(L, R, tid);
+    }
+
+    EdgePair merge_strips(int s0, int s1, int depth, int tid) {
+        if (s1 - s0 == 1) return strips_[s0];
+        const int mid = (s0 + s1) / 2;
+        EdgePair L, R;
+        if (depth < par_levels_) {
+            // the right half on its own thread (free list tid_r), the left half on this one
+            const int tid_r = tid + (1 << (par_levels_ - 1 - depth));
+            std::thread th([&] { R = merge_strips(mid, s1, depth + 1, tid_r); });
+            L = merge_strips(s0, mid, depth + 1, tid);
+            th.join();
+            pool_[tid].free.insert(pool_[tid].free.end(), pool_[tid_r].free.begin(), pool_[tid_r].free.end());
+            pool_[tid_r].free.clear();
+        } else {
+            L = merge_strips(s0, mid, depth + 1, tid);
+            R = merge_strips(mid, s1, depth + 1, tid);
+        }
+        return merge(L, R, tid);
+    }
+
+    // the merge step of Guibas & Stolfi: L's points all precede R's in the cut's frame
+    EdgePair merge(EdgePair L, EdgePair R, int tid) {
+        if (L.le < 0 || R.le < 0 || overflow_.load()) return {-1, -1};
+        int ldo = L.le, ldi = L.re, rdi = R.le, rdo = R.re;
+        for (;;) {                                           // lower common tangent
+            if (leftof(org(rdi), ldi)) ldi = lnext(ldi);
+            else if (rightof(org(ldi), rdi)) rdi = rprev(rdi);
+            else break;
+        }
+        int basel = connect(tid, sym(rdi), ldi);
+        if (basel < 0) return {-1, -1};
+        if (org(ldi) == org(ldo)) ldo = sym(basel);
+        if (org(rdi) == org(rdo)) rdo = basel;
+        for (;;) {                                           // the rising bubble
+            int lcand = onext(sym(basel));
+            if (rightof(dest(lcand), basel)) {
+                while (in_circle(dest(basel), org(basel), dest(lcand), dest(onext(lcand)))) {
+                    const int t = onext(lcand);
+                    remove(tid, lcand);
+                    lcand = t;
+                }
+            }
+            int rcand = oprev(basel);
+            if (rightof(dest(rcand), basel)) {
+                while (in_circle(dest(basel), org(basel), dest(rcand), dest(oprev(rcand)))) {
+                    const int t = oprev(rcand);
+                    remove(tid, rcand);
+                    rcand = t;
+                }
+            }
+            const bool lval = rightof(dest(lcand), basel), rval = rightof(dest(rcand), basel);
+            if (!lval && !rval) break;
+            if (!lval || (rval && in_circle(dest(lcand), org(lcand), org(rcand), dest(rcand))))
+                basel = connect(tid, rcand, sym(basel));
+            else
+                basel = connect(tid, sym(basel), sym(lcand));
+            if (basel < 0) return {-1, -1};
+        }
+        return {ldo, rdo};
+    }
+
+    const std::vector<Pt>& p_;
+    int n_;
+    size_t cap_ = 0;
+    std::vector<int> onext_, org_, order_, strip_lo_;
+    std::vector<EdgePair> strips_;
+    std::vector<unsigned char> alive_;
+    std::atomic<size_t> next_{0};
+    std::atomic<bool> overflow_{false};
+    // per task: its free quads and its pool range, each on its own cache lines (adjacent, every make_edge of one
+    // thread invalidated the others' lines)
+    struct alignas(128) TaskPool {
+        std::vector<int> free;
+        size_t bump = 0, end = 0;
+    };
+    TaskPool pool_[16];
+    size_t merge_base_ = 0;
+    int par_levels_ = 0;
+};
+
+// DelaunayTriangulation's triangles (ACMMP.cpp:932-955) in triangles()' order: the divide-and-conquer form, or
+// the incremental one when that declines
+std::vector<std::array<int, 3>> delaunay_triangles(const std::vector<Pt>& pts, long long extent) {
+    if (!std::getenv("ACMMP_DELAUNAY_INCREMENTAL")) {
+        DelaunayDC dc(pts);
+        if (dc.run()) return dc.triangles();
+    }
+    Delaunay d(pts, extent);
+    d.run();
+    return d.triangles();
+}
+
 // Get3DPointonRefCam (ACMMP.cpp:287-312), float maths with the reference's promotions
 void point_on_ref_cam(int x, int y, float depth, const acmmp_camera& c, float out[3]) {
     if (c.model == ACMMP_SPHERE) {
@@ -378,9 +700,7 @@ acmmp_status acmmp_delaunay(const int* xy, int n, int W, int H, int* tri_xy, int
     if (n == 0) return ACMMP_OK;                           // ACMMP.cpp:934-936
     std::vector<Pt> pts(n);
     for (int i = 0; i < n; ++i) pts[i] = {xy[2 * i], xy[2 * i + 1]};
-    Delaunay d(pts, std::max<long long>(std::max(W, H), 1));
-    d.run();
-    const auto tris = d.triangles();
+    const auto tris = delaunay_triangles(pts, std::max<long long>(std::max(W, H), 1));
     const int m = static_cast<int>(tris.size());
     for (int k = 0; k < std::min(m, cap); ++k)
         for (int j = 0; j < 3; ++j) {
@@ -491,9 +811,7 @@ acmmp_status planar_triangles_pts(const acmmp_camera& cam, const std::vector<int
     if (n > 0) {                                           // triangulate once (ACMMP.cpp:932-955)
         std::vector<Pt> pts(n);
         for (int i = 0; i < n; ++i) pts[i] = {xy[2 * i], xy[2 * i + 1]};
-        Delaunay dl(pts, std::max<long long>(std::max(W, H), 1));
-        dl.run();
-        for (const auto& t : dl.triangles()) {
+        for (const auto& t : delaunay_triangles(pts, std::max<long long>(std::max(W, H), 1))) {
             bool inside = true;
             for (int j = 0; j < 3; ++j) {
                 const int x = xy[2 * t[j]], y = xy[2 * t[j] + 1];

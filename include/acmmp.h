@@ -240,6 +240,14 @@ acmmp_status acmmp_band_halo_ranges(const acmmp_ctx *ctx, int ranges[8]);
 /* In-process exchange: copy rows [row_a, row_b) of `colour`'s current plane / cost / selected-view
  * state from src to dst (same or peer device; waits for src's stream). */
 acmmp_status acmmp_band_copy_rows(acmmp_ctx *dst, acmmp_ctx *src, int colour, int row_a, int row_b);
+/* Host transport of the same exchange (ranks without a device-to-device path, e.g. a gloo or MPI run):
+ * rows [row_a, row_b) of `colour`'s current state to / from host buffers of (row_b - row_a) * ceil(W / 2)
+ * colour-grid pixels -- planes 4 floats, costs 1 float, selected-view masks 1 uint32 each.  get waits for the
+ * context's half-sweep; set is complete on return. */
+acmmp_status acmmp_band_get_rows(acmmp_ctx *ctx, int colour, int row_a, int row_b, float *planes, float *costs,
+                                 uint32_t *selected_views);
+acmmp_status acmmp_band_set_rows(acmmp_ctx *ctx, int colour, int row_a, int row_b, const float *planes,
+                                 const float *costs, const uint32_t *selected_views);
 /* GetDepthandNormal + the two filters on band +- 10 / 5 rows; synchronous.  Rows [row0, row1) of the
  * row-major outputs (acmmp_download / acmmp_device_outputs) are then final. */
 acmmp_status acmmp_band_end(acmmp_ctx *ctx, int do_post);

@@ -7,6 +7,8 @@ The RCCL transport of the same ranges (acmmp_comm_band_exchange) needs one GPU p
 multi-GPU bench.  Covered: pinhole and SPHERE, 2-4 bands, the reference's uncovered last row (odd H with
 floor(H/2) a multiple of 16), exact and fast math, a geometric-consistency pass on reloaded state, and
 the raw state without post-processing.  Tolerance: none (NaNs compared as NaN)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -200,3 +202,46 @@ def test_bench_band_split_single_rank(monkeypatch):
         dist.destroy_process_group()
     assert "error" not in out, out
     assert out["bit_identical_to_whole_view"] and out["bands"] == [(0, 96)] and out["ms_per_depth_map"] > 0
+
+
+def _host_rank(rank, world, port, kind, W, H, V, math, out_dir):
+    """One rank of a band run in its own process, both on GPU 0, the halo through host memory over gloo."""
+    import os
+
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        sc = _scene(kind, W, H, V, seed=W + H + V)
+        p = _params(sc)
+        with capi.Context(0) as ctx:
+            _setup(ctx, sc, p, math)
+            lo, hi = band.run_rank_host(ctx, 2025, H, rank, world, band.gloo_exchange)
+            got = _outputs(ctx)
+        with capi.Context(0) as full:
+            _setup(full, sc, p, math)
+            full.run_patchmatch(2025)
+            want = _outputs(full)
+        for g, w, name in zip(got, want, ("planes", "costs", "selected_views")):
+            assert_bitwise_equal(g[lo:hi], w[lo:hi], f"rank {rank} {name} rows [{lo}, {hi})")
+        open(os.path.join(out_dir, f"rank{rank}.ok"), "w").write(f"{lo} {hi}\n")
+    finally:
+        dist.destroy_process_group()
+
+
+HOST_CASES = [("sphere", 160, 96, 3, 2, "fast"), ("pinhole", 96, 97, 3, 3, "exact")]
+
+
+@pytest.mark.parametrize("kind,W,H,V,world,math", HOST_CASES,
+                         ids=[f"{k}-{w}x{h}-v{v}-w{n}-{m}" for k, w, h, v, n, m in HOST_CASES])
+def test_bands_over_processes_with_host_transport(tmp_path, kind, W, H, V, world, math):
+    """The band protocol across processes: `world` ranks, each its own process with its own context on GPU 0,
+    the halo rows after every half-sweep through host buffers over gloo (band.run_rank_host; the RCCL transport of
+    the same ranges needs one GPU per rank).  Every rank's band equals the whole-view run bit for bit."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_host_rank, args=(world, port, kind, W, H, V, math, str(tmp_path)), nprocs=world, join=True)
+    assert sorted(os.listdir(tmp_path)) == [f"rank{r}.ok" for r in range(world)]

@@ -197,3 +197,61 @@ def test_planar_prior_host_pipeline_matches_restatement():
         exp[j, i] = planes[int(lab[j, i]) - 1]
     assert np.array_equal(prior.view(np.uint32), exp.view(np.uint32))
     assert (masks > 0).mean() > 0.5
+
+
+def _locally_delaunay(tri):
+    """A triangulation (n, 3, 2) of integer points tiles its hull and is Delaunay iff every interior edge is
+    locally Delaunay: the far vertex of the triangle across it lies on or outside the circumcircle (exact
+    integer arithmetic in Python ints)."""
+    edges = {}
+    for k, t in enumerate(tri.tolist()):                     # Python ints: no fixed-width overflow below
+        for j in range(3):
+            a, b = tuple(t[(j + 1) % 3]), tuple(t[(j + 2) % 3])
+            edges[(a, b)] = (k, tuple(t[j]))
+    for (a, b), (k, c) in edges.items():
+        other = edges.get((b, a))
+        if other is None:
+            continue
+        d = other[1]
+        # in-circle of d against the CCW triangle (a, b, c)
+        adx, ady, bdx, bdy, cdx, cdy = a[0] - d[0], a[1] - d[1], b[0] - d[0], b[1] - d[1], c[0] - d[0], c[1] - d[1]
+        det = ((adx * adx + ady * ady) * (bdx * cdy - bdy * cdx) - (bdx * bdx + bdy * bdy) * (adx * cdy - ady * cdx)
+               + (cdx * cdx + cdy * cdy) * (adx * bdy - ady * bdx))
+        if det > 0:
+            return False
+    return True
+
+
+@pytest.mark.parametrize("layout", ["support", "grid", "general"])
+@pytest.mark.parametrize("threads", ["1", "8"])
+def test_divide_and_conquer_delaunay(monkeypatch, layout, threads):
+    """The divide-and-conquer triangulation (Dwyer strips, parallel merges) on support-point layouts big enough
+    to take its threaded path: a Delaunay triangulation of the hull (Euler count, orientation, local Delaunay
+    edges, area), independent of the thread count, and -- points in general position, where the Delaunay
+    triangulation is unique -- the incremental form's triangles exactly (ACMMP_DELAUNAY_INCREMENTAL)."""
+    rng = np.random.default_rng(11)
+    if layout == "support":
+        W, H = 1000, 600
+        pts = [(c + rng.integers(0, 5), r + rng.integers(0, 5)) for c in range(0, W, 5) for r in range(0, H, 5)
+               if rng.random() < 0.4]
+    elif layout == "grid":
+        W, H = 600, 400
+        pts = [(c, r) for c in range(0, W, 5) for r in range(0, H, 5)]                  # co-circular everywhere
+    else:
+        W, H = 16000, 16000
+        pts = list({(int(x), int(y)) for x, y in rng.integers(0, W, (12000, 2))})
+    pts = np.array(pts, np.int32)
+    monkeypatch.setenv("ACMMP_DELAUNAY_THREADS", threads)
+    tri = capi.delaunay(pts, W, H)
+    monkeypatch.setenv("ACMMP_DELAUNAY_THREADS", "3")
+    again = capi.delaunay(pts, W, H)
+    np.testing.assert_array_equal(tri, again)                   # the thread count does not change the result
+    assert len(tri) == 2 * len(pts) - 2 - _hull_size(pts)
+    t = tri.astype(np.int64)
+    orient = (t[:, 1, 0] - t[:, 0, 0]) * (t[:, 2, 1] - t[:, 0, 1]) - (t[:, 1, 1] - t[:, 0, 1]) * (t[:, 2, 0] - t[:, 0, 0])
+    assert (orient > 0).all()
+    assert int(orient.sum()) == _area2(_hull(pts, False))
+    assert _locally_delaunay(tri)
+    if layout == "general":
+        monkeypatch.setenv("ACMMP_DELAUNAY_INCREMENTAL", "1")
+        np.testing.assert_array_equal(capi.delaunay(pts, W, H), tri)
