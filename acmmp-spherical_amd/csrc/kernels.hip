@@ -1241,7 +1241,7 @@ __device__ __forceinline__ float4 perturbed_normal(float4 v, float4 n, Rng& rs, 
 // ------------------------------------------------------------------ cost-vector helpers
 
 // Evaluate all source views of plane `ph` and hand each cost to f(view0, cost) in view order.
-template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM, typename F>
+template <int MODEL, int VB, int STAGED, bool PIPE, int TEX, int FM, bool NOFULL = false, typename F>
 __device__ __forceinline__ void for_all_views_t(const KParams& kp, int px, int py, const Patch& pt, float4 ph,
                                                 uint32_t wave_mask, F&& f, uint32_t fixkey = kFixNone) {
     int v = 0;
@@ -1263,7 +1263,11 @@ __device__ __forceinline__ void for_all_views_t(const KParams& kp, int px, int p
         }
         if (nv == 0) break;
         float cost[VB];
-        if ((MODEL == kSphere ? VB <= 2 : true) && VB > 1 && nv == VB)
+        // (NOFULL: not in k_eval_nb's interpolating instances, whose views are a loop anyway -- the second copy
+        // of the chunk took the 2-view one, V = 2, to 371 spilled dwords at its 6-wave budget)
+        constexpr bool kFullCopy = (MODEL == kSphere ? VB <= 2 : true) && VB > 1 &&
+                                   !(NOFULL && MODEL == kSphere && STAGED == 3 && FM && TEX == 1);
+        if (kFullCopy && nv == VB)
             ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM, true>(kp, px, py, pt, ph, vlist, nv, cost, fixkey);
         else
             ncc_chunk<MODEL, VB, STAGED, PIPE, TEX, FM>(kp, px, py, pt, ph, vlist, nv, cost, fixkey);
@@ -1840,17 +1844,22 @@ __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour
 
 #endif  // ACMMP_IN_TU(0)
 
-// k_eval_nb register budgets (minimum waves per SIMD): SPHERE exact 8, SPHERE fast 7 (72 VGPRs, no
-// spills; r02 A/B: 7 waves +0.6% over 8), pinhole none.
+// k_eval_nb register budgets (minimum waves per SIMD): SPHERE exact 8, SPHERE fast 6 (below), pinhole fast 6.
 // TEX (binary16 texels) and FM (fast math) are compile-time here, so each of the four variants gets its
 // own register allocation (a runtime branch between them sized every variant for the largest: 23
 // VGPRs spilled at the 64-VGPR budget; r02 A/B profiles/r02_split_nb_ab.txt: fast 388 -> 394, exact
 // 316.6 -> 320 Mpixel-iterations/s)
 // fast pinhole: 6 waves (80 VGPRs, 5 dwords spilled outside the sample loops) against 5 unconstrained (90):
-// C2 k_eval_nb 3.233 -> 3.212 ms (profiles/r04_ab5_ab.txt)
+// C2 k_eval_nb 3.233 -> 3.212 ms (profiles/r04_ab5_ab.txt).  A software-pipelined form of its sample loop (the
+// next sample's gathers issued before the current one is accumulated: 96 VGPRs, 5 waves) measured 3.17 -> 3.30 ms
+// (round 5, profiles/r05_ab3_ab.txt): not kept.
 template <int MODEL, int VB, int TEX, int FM>
 #ifndef ACMMP_NB_SPH_WAVES
-#define ACMMP_NB_SPH_WAVES 7   // 6: no spills (writes 0.49 -> 0.20 GB per launch) but +3% time, profiles/r04_ab8_ab.txt
+// fast SPHERE: 6 waves (80 VGPRs, no spills).  Round 4's form (all 16 nodes of a view live at once) spilled 9 dwords at
+// 7 waves and was 3% slower at 6; with the node-column form and no prologue values kept across the view loop
+// (ncc_chunk), 6 waves beat 7: k_eval_nb 1.545 -> 1.511 ms at the metric, C3 15.69 -> 15.30 ms
+// (profiles/r05_ab3_ab.txt)
+#define ACMMP_NB_SPH_WAVES 6
 #endif
 __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_SPH_WAVES : 8) : (FM ? 6 : 1)) void k_eval_nb(
     const KParams kp, const int colour) {
@@ -1877,7 +1886,7 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_SPH_WAVES : 
     // The output address and the fallback key are formed from it and the lane id where they are used.
     const uint32_t wbase = static_cast<uint32_t>(uniform_int(static_cast<int>(kp.row_lo * kp.Wh + blockIdx.x * kNbPix + (t >> 6) * 8)));
     const uint32_t fixkey = kp.nbfix ? wbase : kFixNone;
-    for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
+    for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM, true>(
         kp, px, py, pt, ph, all, [&](int v, float c) {
             const int l = lane_id_here();
             kp.hyp_cost[(static_cast<long long>(l & 7) * kp.V + v) * Pc + (wbase + (l >> 3))] = c;
@@ -2904,7 +2913,7 @@ __global__ __launch_bounds__(256) void k_debug_nb(const KParams kp, int n, const
     float* o = out + k * kp.V;
     const uint32_t all = kp.V >= 32 ? 0xFFFFFFFFu : ((1u << kp.V) - 1u);
     const uint32_t fixkey = kp.nbfix ? static_cast<uint32_t>(uniform_int(static_cast<int>(blockIdx.x * kNbPix + (t >> 6) * 8))) : kFixNone;
-    for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM>(
+    for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM, true>(
         kp, px, py, pt, ph, all, [&](int v, float c) { o[v] = c; }, fixkey);
 }
 

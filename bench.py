@@ -246,9 +246,14 @@ def cpu_baseline(args, sc, params, gpu_rate_check=None):
         rows_done += rows_per_band
         bands.append(rows_per_band)
     pix_iter = rows_done * args.width * args.iters
+    rate = pix_iter / t_sum                                  # pixel-iterations per second
     return {
-        "value": round(pix_iter / t_sum / 1e6, 5),
+        "value": round(rate / 1e6, 5),
         "unit": "Mpixel-iterations/s",
+        # the same rate as time per depth map of the whole view (H x W pixels x iterations), beside the GPU's
+        # ms_per_depth_map; the reference itself cannot be built here (nvcc, OpenCV: DESIGN.md §3), so this is
+        # its restatement's rate on the box's cores
+        "ms_per_depth_map": round(args.width * args.height * args.iters / rate * 1e3, 1),
         "cores": threads,
         "kind": "port",
         "sample": f"{nb} bands of {'/'.join(map(str, bands))} rows of the same {args.width}x{args.height} {args.model} view "

@@ -3,7 +3,8 @@ planes / costs, or compare the saved outputs of several builds bit for bit.
 
   python scripts/ab_bitident.py run OUT.npz [--math fast|exact]     (in a process with ACMMP_LIB set)
   python scripts/ab_bitident.py cmp A.npz B.npz ...
-Scenes: the bench metric (2000x1500 V=4), 3200x1600 V=15 (C3 size, view-chunked) and a small 640x320 V=4."""
+Scenes: the bench metric (2000x1500 V=4), 3200x1600 V=15 (C3 size, view-chunked), a small 640x320 V=4 and the C2
+pinhole rig (1600x1200 V=10)."""
 import os
 import sys
 
@@ -11,14 +12,15 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "acmmp-spherical_amd"))
 import numpy as np  # noqa: E402
 
-CASES = [(2000, 1500, 4, 1235), (3200, 1600, 15, 7), (640, 320, 4, 3)]
+CASES = [(2000, 1500, 4, 1235), (3200, 1600, 15, 7), (640, 320, 4, 3), (1600, 1200, 10, 9)]
 
 
 def run(out, math):
     from acmmp import capi, scene, types
     res = {}
     for (W, H, V, seed) in CASES:
-        sc = scene.sphere_scene(W, H, n_src=V, seed=seed)
+        sc = (scene.pinhole_scene(W, H, n_src=V, seed=seed) if (W, H, V) == (1600, 1200, 10)
+              else scene.sphere_scene(W, H, n_src=V, seed=seed))
         c0 = sc.cameras[0]
         p = types.default_params(num_images=len(sc.images), depth_min=float(c0["depth_min"]) * 0.6,
                                  depth_max=float(c0["depth_max"]) * 1.2)

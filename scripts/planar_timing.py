@@ -27,6 +27,10 @@ out = {"size": [W, H], "model": model}
 t = time.perf_counter(); xy = capi.support_points(costs); out["support_points_ms_x2"] = (time.perf_counter() - t) * 1e3
 out["n_support"] = int(len(xy))
 t = time.perf_counter(); tri = capi.delaunay(xy, W, H); out["delaunay_ms"] = (time.perf_counter() - t) * 1e3
+os.environ["ACMMP_DELAUNAY_INCREMENTAL"] = "1"              # the incremental form, for comparison
+t = time.perf_counter(); tri_inc = capi.delaunay(xy, W, H); out["delaunay_incremental_ms"] = (time.perf_counter() - t) * 1e3
+del os.environ["ACMMP_DELAUNAY_INCREMENTAL"]
+out["same_triangles_as_incremental"] = bool(np.array_equal(tri, tri_inc))
 out["n_tri"] = int(len(tri))
 t = time.perf_counter(); capi.planar_prior_host(c0, depth, costs, float(p["depth_min"]), float(p["depth_max"]))
 out["planar_prior_host_ms"] = (time.perf_counter() - t) * 1e3

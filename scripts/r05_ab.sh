@@ -13,7 +13,8 @@ if [ -z "$NO_BITIDENT" ]; then
     ACMMP_LIB=$lib timeout -k 10 400 python scripts/ab_bitident.py run $OUT/$n.npz --math fast > $OUT/bi_$n.log 2>&1 || { echo "bitident $n failed"; tail $OUT/bi_$n.log; exit 1; }
     NP="$NP $OUT/$n.npz"
   done
-  python scripts/ab_bitident.py cmp $NP
+  python scripts/ab_bitident.py cmp $NP | tee $OUT/bitident.txt
+  rm -f $NP                                            # (large: gpurun copies back at most 64 MiB)
 fi
 for cfg in "$@"; do
   for r in $(seq $REPS); do
