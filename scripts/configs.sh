@@ -22,5 +22,5 @@ if [ "$2" != "no-pmc" ]; then
 fi
 run c2_patchmatch 300 python bench.py $C2 --no-cpu-baseline --no-variant --no-pipeline --pmc $OUT/pmc_c2.json
 run c3_patchmatch 400 python bench.py $C3 --steps 3 --warmup 1 --no-cpu-baseline --no-variant --no-pipeline --pmc $OUT/pmc_c3.json
-run c2_pipeline 500 python -u scripts/pipeline_bench.py --model pinhole --width 1600 --height 1200 --views 49 --n-src 10
+run c2_pipeline 500 python -u scripts/pipeline_bench.py --model pinhole --width 1600 --height 1200 --views 49 --n-src 10 --math fast
 echo CONFIGS_DONE
