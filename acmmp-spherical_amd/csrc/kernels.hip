@@ -1937,8 +1937,10 @@ __device__ __forceinline__ float fix_fold(const float4* smp) {
     return ncc_cost(pt.sbw, (f32x2){pt.sref, pt.srr}, ssrs, sss);
 }
 
-// block b of the fix grid takes region b % kNbFixRegions, its (b / kNbFixRegions)-th stripe of entries
-template <int TEX>
+// block b of the fix grid takes region b % kNbFixRegions, its (b / kNbFixRegions)-th stripe of entries.
+// REF: the refinement's entries (k_eval_ref's queue, the same buffer after k_eval_nb's is drained): hypothesis h is
+// candidate h (kp.cand), the cost goes to its cost vector (kp.cand_vcost).
+template <int TEX, bool REF = false>
 __global__ __launch_bounds__(256) void k_nb_fix(const KParams kp, const int colour) {
     __shared__ float4 smp[kFixPerBlock][36];
     const int t = threadIdx.x, l = t & 63;
@@ -1961,10 +1963,10 @@ __global__ __launch_bounds__(256) void k_nb_fix(const KParams kp, const int colo
             v = static_cast<int>(key & 31u);
             const int py = static_cast<int>(ci / kp.Wh);
             const int px = 2 * static_cast<int>(ci - static_cast<long long>(py) * kp.Wh) + ((py + colour) & 1);
-            fix_row<TEX>(kp, px, py, plane_at(kp, kp.nbpos[h * Pc + ci]), v, j, smp[e]);
+            fix_row<TEX>(kp, px, py, REF ? kp.cand[h * Pc + ci] : plane_at(kp, kp.nbpos[h * Pc + ci]), v, j, smp[e]);
         }
         __syncthreads();
-        if (act && j == 0) kp.hyp_cost[(static_cast<long long>(h) * kp.V + v) * Pc + ci] = fix_fold(smp[e]);
+        if (act && j == 0) (REF ? kp.cand_vcost : kp.hyp_cost)[(static_cast<long long>(h) * kp.V + v) * Pc + ci] = fix_fold(smp[e]);
         __syncthreads();
     }
 }
@@ -2389,7 +2391,33 @@ __global__ __launch_bounds__(256, (MODEL == kSphere && VB > 4 && TF == 2) ? ACMM
     const PixState& st = kp.pst[ci];
     const bool done = !(st.flags & 1u) && !(partial < st.cost_now);
     kp.cand_cost[h * Pc + ci] = done ? partial : temp_cost;
-    if (kRefInterp && !done) kp.cand_rough[h * Pc + ci] = rough & mask;   // the tail's restart views
+    if constexpr (kRefInterp) {
+        // a survivor's selected views that fell back: queued (pixel << 8 | candidate << 5 | view, the buffer and
+        // regions of k_eval_nb's queue, drained before) for k_nb_fix<TEX, true>, which writes their per-sample
+        // costs into the candidate's cost vector before the tail runs; the tail restarts the chain
+        // (round 5's first form evaluated them in the tail itself: every lane of a tail wave then took every
+        // other lane's fallback views, and the tail moved 20 GB per launch at C3 with 48% L2 hits)
+        const uint32_t need = done ? 0u : (rough & mask);
+        if (!done) kp.cand_rough[h * Pc + ci] = need;
+        const unsigned long long any = __ballot(need != 0u);
+        if (any) {
+            const int lane = lane_id_here();
+            const unsigned region = blockIdx.x % kNbFixRegions;
+            for (int v = 0; v < S; ++v) {
+                const bool redo = (need >> v) & 1u;
+                const unsigned long long b = __ballot(redo);
+                if (!b) continue;
+                const int leader = __ffsll(static_cast<long long>(b)) - 1;
+                unsigned base = 0u;
+                if (lane == leader) base = atomicAdd(kp.nbfix_count + region, static_cast<unsigned>(__popcll(b)));
+                base = __builtin_amdgcn_readlane(base, leader);
+                const unsigned slot = base + static_cast<unsigned>(__popcll(b & ((1ull << lane) - 1ull)));
+                if (redo && slot < kp.nbfix_cap)
+                    kp.nbfix[static_cast<long long>(region) * kp.nbfix_cap + slot] =
+                        (static_cast<uint32_t>(ci) << 8) | (static_cast<uint32_t>(h) << 5) | static_cast<uint32_t>(v);
+            }
+        }
+    }
     const unsigned long long b = __ballot(!done);
     if (b) {                                                 // queue the wave's survivors in the block's slots
         const int lane = __lane_id();
@@ -2481,12 +2509,12 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
         const float weight_norm = st.weight_norm;
         const uint32_t vwp[4] = {vw.x, vw.y, vw.z, vw.w};
         // k_eval_ref's interpolated instance (SPHERE V > 4, fast, binary16) left out the selected views of
-        // [0, S) whose interpolation nodes spread too far (`need`): they are evaluated here with every sample
-        // projected, and the candidate's chain restarts from view 0, folding k_eval_ref's stored costs of its
-        // other views in view order -- the chain k_eval_ref would have formed with the per-sample costs there
+        // [0, S) whose interpolation nodes spread too far (`need`); k_nb_fix<TEX, true> has since written their
+        // per-sample costs into the cost vector, so such a candidate's chain restarts from view 0 over the stored
+        // costs of [0, S) in view order -- the chain k_eval_ref would have formed with the per-sample costs there
         constexpr bool kRefInterp = MODEL == kSphere && VB > 4 && TF == 2;
         const uint32_t need = kRefInterp ? kp.cand_rough[h * Pc + ci] : 0u;
-        uint32_t mask = need;
+        uint32_t mask = 0u;
         for (int v = S; v < kp.V; ++v) if (vw_get(vwp, v) > 0.0f) mask |= 1u << v;
         const uint32_t umask = wave_or(mask, kp.V);
         const float4 dc = ray_at<MODEL>(kp, px, py);
@@ -2504,11 +2532,8 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
                 else temp_cost = fmaf(w, c, temp_cost);
             }
         };
-        int nxt = need ? 0 : S;                              // restart: next stored view of [0, S) to fold
-        auto fold_stored = [&](int upto) {
-            for (; nxt < upto; ++nxt)
-                if (!((need >> nxt) & 1u)) add_term(nxt, vcost[nxt * Pc]);
-        };
+        if (kRefInterp && need)
+            for (int v = 0; v < S; ++v) add_term(v, vcost[v * Pc]);
         // SPHERE V > 4: 4-view chunks (87 VGPRs, 5 waves) -- each chunk recomputes the 36 samples' rays,
         // weights and reference texels, so fewer chunks save that work: C3 k_eval_ref + tail 10.52 -> 9.03 ms
         // against 2-view chunks (74 VGPRs, 6 waves), +5.4% (profiles/r04_ab6_ab.txt)
@@ -2521,12 +2546,9 @@ __global__ __launch_bounds__(256) void k_eval_ref_tail(const KParams kp, const i
         constexpr int VBT = (MODEL == kSphere && VB > 4) ? ACMMP_TAIL_SPH_VB
                           : (MODEL == kPinhole && VB > 4) ? ACMMP_TAIL_PIN_VB : ref_vb<MODEL, VB>();
         for_all_views_tf<MODEL, VBT, 0, kRefPipe, TF>(kp, px, py, pt, tp, umask, [&](int v, float c) {
-            if (kRefInterp && v < S && !((need >> v) & 1u)) return;     // another lane's restart view
-            if (kRefInterp && need) fold_stored(v < S ? v : S);
             vcost[v * Pc] = c;
             add_term(v, c);
         });
-        if (kRefInterp && need) fold_stored(S);
         kp.cand_cost[h * Pc + ci] = temp_cost / weight_norm;
     }
 }
@@ -3025,8 +3047,14 @@ hipError_t launch_eval_ref(const KParams& kp0, int colour, hipStream_t s) {
     hipError_t e = hipSuccess;
     const dim3 grd_ref = static_cast<unsigned>(cdiv(npix, kRefPix));
     if (kp.ref_split > 0 && (e = hipMemsetAsync(kp.surv_count, 0, sizeof(unsigned) * grd_ref.x, s)) != hipSuccess) return e;
+    // the interpolated instance (fast SPHERE, V > 4) queues its survivors' fallback views on k_eval_nb's queue
+    // (drained by then): a region's k_eval_ref blocks x 255 candidates x S views fit its room (Pc S / 51 against
+    // k_eval_nb's Pc x chunk / 32, S <= chunk)
+    const bool ref_fix = kp.interp && kp.nbfix && kp.model == kSphere && kp.fast && kp.tex16 && kp.V > 4;
+    if (ref_fix && (e = hipMemsetAsync(kp.nbfix_count, 0, sizeof(unsigned) * kNbFixRegions, s)) != hipSuccess) return e;
     if (kp.geom) ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, true, TF><<<grd_ref, 256, lds_ref, s>>>(kp, colour))));
     else ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref<M, VBC, false, TF><<<grd_ref, 256, lds_ref, s>>>(kp, colour))));
+    if (ref_fix) k_nb_fix<1, true><<<16 * kNbFixRegions, 256, 0, s>>>(kp, colour);
     if (kp.ref_split > 0) {
         // the survivors' prefix over k_eval_ref blocks, then 8 x nk tail blocks (the queue's length is
         // known on the device only: nk covers the largest possible queue, up to 256 blocks per XCD)
