@@ -7,7 +7,10 @@ library is missing or no GPU is visible, every call fails loudly.
 from __future__ import annotations
 
 import ctypes as C
+import mmap
 import os
+import threading
+import weakref
 
 import numpy as np
 
@@ -16,6 +19,58 @@ from .types import CAMERA_DTYPE, PARAMS_DTYPE
 HERE = os.path.dirname(os.path.abspath(__file__))
 # ACMMP_LIB selects another in-tree build of the same library (A/B experiments); default: the product build
 LIB_PATH = os.environ.get("ACMMP_LIB") or os.path.join(HERE, "libacmmp.so")
+
+class _HostPool:
+    """Recycled page-aligned private mappings for large D2H destinations.  Fresh heap pages made the copy into
+    them crawl (30 ms for a 800x600 view's planes + costs, 0.9 ms into a hugepage mapping,
+    profiles/r05_d2h_probe.json), and a new mapping per download pays its page faults every time: a mapping
+    comes back here when the last array (or view) on it is collected and the next download of that size
+    reuses its resident pages.  At most `cap` bytes are kept."""
+
+    def __init__(self, cap: int = 4 << 30):
+        self.cap, self.held, self.free = cap, 0, {}
+        self.lock = threading.Lock()
+
+    def take(self, n: int):
+        with self.lock:
+            lst = self.free.get(n)
+            if lst:
+                self.held -= n
+                return lst.pop()
+        mm = mmap.mmap(-1, n, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+        if hasattr(mmap, "MADV_HUGEPAGE"):
+            mm.madvise(mmap.MADV_HUGEPAGE)
+        return mm
+
+    def give(self, mm, n: int):
+        # (called while the array still holds its buffer export: an unkept mapping is unmapped when the last
+        # reference goes, not closed here)
+        with self.lock:
+            if self.held + n <= self.cap:
+                self.free.setdefault(n, []).append(mm)
+                self.held += n
+
+
+_POOL = _HostPool()
+
+
+def host_empty(shape, dtype=np.float32) -> np.ndarray:
+    """An uninitialised host array for a D2H copy: arrays of 4 MiB and up live on a 2 MiB aligned private
+    mapping advised MADV_HUGEPAGE from _HostPool (see there); smaller ones are plain np.empty."""
+    dt = np.dtype(dtype)
+    count = int(np.prod(shape))
+    n = count * dt.itemsize
+    if n < (4 << 20):
+        return np.empty(shape, dt)
+    size = (n + (2 << 20) - 1) // (2 << 20) * (2 << 20) + (2 << 20)     # whole 2 MiB pages + alignment slack
+    mm = _POOL.take(size)
+    base = np.frombuffer(mm, np.uint8)
+    off = (-base.ctypes.data) % (2 << 20)
+    del base
+    flat = np.frombuffer(mm, dt, count, off)       # the base every view of the result keeps alive
+    weakref.finalize(flat, _POOL.give, mm, size)
+    return flat.reshape(shape)
+
 
 STATUS = {0: "ok", 1: "invalid argument", 2: "HIP runtime error", 3: "out of device memory",
           4: "call order violated", 5: "unsupported configuration", 6: "no HIP device"}
@@ -365,8 +420,8 @@ class Context:
         return n.value
 
     def download_planar_prior(self):
-        prior = np.empty((self.H, self.W, 4), np.float32)
-        masks = np.empty((self.H, self.W), np.uint32)
+        prior = host_empty((self.H, self.W, 4), np.float32)
+        masks = host_empty((self.H, self.W), np.uint32)
         self._check(self.L.acmmp_download_planar_prior(self.h, _p(prior), _p(masks)), "download_planar_prior")
         return prior, masks
 
@@ -376,8 +431,8 @@ class Context:
                     "run_patchmatch")
 
     def download(self):
-        planes = np.empty((self.H, self.W, 4), np.float32)
-        costs = np.empty((self.H, self.W), np.float32)
+        planes = host_empty((self.H, self.W, 4), np.float32)
+        costs = host_empty((self.H, self.W), np.float32)
         self._check(self.L.acmmp_download(self.h, _p(planes), _p(costs)), "download")
         return planes, costs
 
@@ -405,8 +460,8 @@ class Context:
                     "memcpy D2H")
 
     def download_aux(self):
-        sel = np.empty((self.H, self.W), np.uint32)
-        pre = np.empty((self.H, self.W), np.float32)
+        sel = host_empty((self.H, self.W), np.uint32)
+        pre = host_empty((self.H, self.W), np.float32)
         self._check(self.L.acmmp_download_aux(self.h, _p(sel), _p(pre)), "download_aux")
         return sel, pre
 
@@ -623,7 +678,7 @@ class DeviceBuffer:
         _host_check(self.L.acmmp_memcpy(self.device, C.c_void_p(self.ptr), _p(a), self.nbytes, 0), "memcpy H2D")
 
     def download(self):
-        a = np.empty(self.shape, np.float32)
+        a = host_empty(self.shape, np.float32)
         _host_check(self.L.acmmp_memcpy(self.device, _p(a), C.c_void_p(self.ptr), self.nbytes, 1), "memcpy D2H")
         return a
 

@@ -325,6 +325,7 @@ class PassLog:
     compute_s: float = 0.0            # this rank's ProcessProblem calls of the pass (host wall clock)
     exchange_s: float = 0.0           # the depth-map exchange after it (world > 1)
     exchange_bytes: int = 0           # depth-map bytes every rank holds after the exchange
+    stages: dict = field(default_factory=dict)   # host seconds per stage within the pass (Pipeline.stage_s)
 
 
 class Pipeline:
@@ -371,6 +372,7 @@ class Pipeline:
         # overlap=True means ACMMP_PIPELINE_SLOTS (default 3) contexts; False / 1 = the sequential loop.
         slots = int(os.environ.get("ACMMP_PIPELINE_SLOTS", "3")) if overlap is True else int(overlap or 1)
         self.overlap = slots if (gpu and slots > 1) else 0
+        self.geom_overlap = os.environ.get("ACMMP_PIPELINE_GEOM_OVERLAP", "1") != "0"   # (A/B knob)
         self._extra_engines = []
         self._math = math
         # prepared (padded + binary16) images of every (view, scale), shared by this pipeline's contexts:
@@ -463,14 +465,19 @@ class Pipeline:
         self.log(f"[rank {self.rank}] pass {self.pass_index}: {name}")
         log = PassLog(name)
         t0 = time.perf_counter()
-        if planar and not geom and self.overlap and len(self.my_problems()) > 1:
-            self._pass_overlapped(hier, log)
+        # a planar pass's views are independent; so are a geom pass's when it reads only the previous
+        # pass's depth maps (not multi-geometry, or snapshot order)
+        independent = (planar and not geom) or (geom and self.geom_overlap and (not multi or self.order == "snapshot"))
+        before = dict(self.stage_s)
+        if independent and self.overlap and len(self.my_problems()) > 1:
+            self._pass_overlapped(geom, planar, hier, multi, log)
         else:
             for i in self.my_problems():
                 self.process_problem(i, geom, planar, hier, multi)
                 log.views.append(self.problems[i].ref_image_id)
         self._commit_pending()
         log.compute_s = time.perf_counter() - t0
+        log.stages = {k: v - before.get(k, 0.0) for k, v in self.stage_s.items() if v - before.get(k, 0.0) > 0}
         key = "depths_geom" if geom else "depths"
         if self.world > 1:
             views = [p.ref_image_id for p in self.problems]
@@ -545,13 +552,15 @@ class Pipeline:
         else:
             e.upload_views_device(bufs, cams)
 
-    def _pass_overlapped(self, hier, log):
-        """A planar pass over `self.overlap` engine contexts on the GPU: view k's second half (host planar
-        prior, second RunPatchMatch, store) runs on a worker thread while the main thread runs the next
-        views' first halves on the other contexts -- several views' host planar blocks (Delaunay, on
-        the host as in the reference) in flight at once.  The views of a planar pass are independent
-        (each reads only its own view's earlier-pass state), so the outputs are those of the sequential
-        loop."""
+    def _pass_overlapped(self, geom, planar, hier, multi, log):
+        """A pass over `self.overlap` engine contexts on the GPU: view k's second half runs on a worker
+        thread while the main thread runs the next views' first halves on the other contexts.  In a
+        planar pass the second half is the host planar prior, the second RunPatchMatch and the store
+        (several views' host planar blocks -- Delaunay, on the host as in the reference -- in flight at
+        once); in a geom pass it is the download of the planes and costs and the store, so the next
+        view's kernels run while they copy.  Only passes whose views are independent come here (each
+        reads its own view's earlier-pass state and the previous pass's depth maps), so the outputs are
+        those of the sequential loop."""
         n = self.overlap
         while len(self._extra_engines) < n - 1:
             e = capi.Context(self.device)
@@ -565,7 +574,7 @@ class Pipeline:
                 slot = k % n
                 if busy[slot] is not None:
                     busy[slot].result()                      # the context is free again
-                head = self._problem_head(i, False, True, hier, False, engines[slot])
+                head = self._problem_head(i, geom, planar, hier, multi, engines[slot], defer_download=True)
                 busy[slot] = pool.submit(self._problem_tail, head)
                 log.views.append(self.problems[i].ref_image_id)
             for f in busy:
@@ -576,7 +585,7 @@ class Pipeline:
     def process_problem(self, idx, geom, planar, hier, multi):
         return self._problem_tail(self._problem_head(idx, geom, planar, hier, multi, self.engine))
 
-    def _problem_head(self, idx, geom, planar, hier, multi, e):
+    def _problem_head(self, idx, geom, planar, hier, multi, e, defer_download=False):
         """InuputInitialization, CudaSpaceInitialization and the first RunPatchMatch of ProcessProblem."""
         prob = self.problems[idx]
         ref = prob.ref_image_id
@@ -599,14 +608,19 @@ class Pipeline:
         run_seed = self.seed + 7919 * self.pass_index + 31 * ref
         with self._timed("patchmatch"):
             e.run_patchmatch(run_seed)
-            # a planar pass's first run feeds only the planar block, which a GPU context takes from HBM
-            planes, costs = (None, None) if (planar and self._state_planar(e)) else e.download()
+            # a planar pass's first run feeds only the planar block, which a GPU context takes from HBM;
+            # an overlapped geom pass downloads in the second half
+            skip = (planar and self._state_planar(e)) or (defer_download and not planar)
+            planes, costs = (None, None) if skip else e.download()
         return dict(e=e, p=p, c0=c0, ref=ref, geom=geom, planar=planar, run_seed=run_seed, planes=planes, costs=costs)
 
     def _problem_tail(self, st):
         """The planar block (main.cpp:113-187) with its second RunPatchMatch, and the stores."""
         e, p, c0, ref, geom, planar, run_seed = (st[k] for k in ("e", "p", "c0", "ref", "geom", "planar", "run_seed"))
         planes, costs = st["planes"], st["costs"]
+        if planes is None and not planar:
+            with self._timed("download"):
+                planes, costs = e.download()
         if planar:                                                   # main.cpp:113-187
             p["planar_prior"] = 1
             if self._state_planar(e):

@@ -867,8 +867,8 @@ acmmp_status acmmp_download_planar_prior(acmmp_ctx* c, float* prior, uint32_t* m
     if (!c->has_prior) return fail(c, ACMMP_ERR_STATE, "no planar prior set since the last upload_views");
     HIP_TRY(c, hipSetDevice(c->device));
     const size_t P = P_of(c);
-    if (prior) HIP_TRY(c, hipMemcpy(prior, c->d_prior, sizeof(float4) * P, hipMemcpyDeviceToHost));
-    if (masks) HIP_TRY(c, hipMemcpy(masks, c->d_mask, sizeof(uint32_t) * P, hipMemcpyDeviceToHost));
+    if (prior) HIP_TRY(c, d2h(prior, c->d_prior, sizeof(float4) * P));
+    if (masks) HIP_TRY(c, d2h(masks, c->d_mask, sizeof(uint32_t) * P));
     return ACMMP_OK;
 }
 
@@ -1261,9 +1261,9 @@ acmmp_status acmmp_band_get_rows(acmmp_ctx* c, int colour, int row_a, int row_b,
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));            // the half-sweep that wrote them is complete
     const size_t off = static_cast<size_t>(row_a) * b.Wh, n = static_cast<size_t>(row_b - row_a) * b.Wh;
-    HIP_TRY(c, hipMemcpy(planes, b.plane + off, sizeof(float4) * n, hipMemcpyDeviceToHost));
-    HIP_TRY(c, hipMemcpy(costs, b.cost + off, sizeof(float) * n, hipMemcpyDeviceToHost));
-    HIP_TRY(c, hipMemcpy(sel, b.sel + off, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
+    HIP_TRY(c, d2h(planes, b.plane + off, sizeof(float4) * n));
+    HIP_TRY(c, d2h(costs, b.cost + off, sizeof(float) * n));
+    HIP_TRY(c, d2h(sel, b.sel + off, sizeof(uint32_t) * n));
     return ACMMP_OK;
 }
 
@@ -1314,8 +1314,8 @@ acmmp_status acmmp_download(acmmp_ctx* c, float* planes, float* costs) {
     if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "nothing to download");
     HIP_TRY(c, hipSetDevice(c->device));
     const size_t P = P_of(c);
-    if (planes) HIP_TRY(c, hipMemcpy(planes, c->d_planes_rm, sizeof(float4) * P, hipMemcpyDeviceToHost));
-    if (costs) HIP_TRY(c, hipMemcpy(costs, c->d_costs_rm, sizeof(float) * P, hipMemcpyDeviceToHost));
+    if (planes) HIP_TRY(c, d2h(planes, c->d_planes_rm, sizeof(float4) * P));
+    if (costs) HIP_TRY(c, d2h(costs, c->d_costs_rm, sizeof(float) * P));
     return ACMMP_OK;
 }
 
@@ -1324,8 +1324,8 @@ acmmp_status acmmp_download_aux(acmmp_ctx* c, uint32_t* sel, float* pre) {
     if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "nothing to download");
     HIP_TRY(c, hipSetDevice(c->device));
     const size_t P = P_of(c);
-    if (sel) HIP_TRY(c, hipMemcpy(sel, c->d_sel_rm, sizeof(uint32_t) * P, hipMemcpyDeviceToHost));
-    if (pre) HIP_TRY(c, hipMemcpy(pre, c->d_pre, sizeof(float) * P, hipMemcpyDeviceToHost));
+    if (sel) HIP_TRY(c, d2h(sel, c->d_sel_rm, sizeof(uint32_t) * P));
+    if (pre) HIP_TRY(c, d2h(pre, c->d_pre, sizeof(float) * P));
     return ACMMP_OK;
 }
 
@@ -1381,7 +1381,7 @@ acmmp_status acmmp_jbu(acmmp_ctx* c, const float* ref, int W, int H, const float
     if (e == hipSuccess) e = hipMemcpy(d_coarse, coarse, sizeof(float) * p, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = launch_jbu(d_ref, W, H, d_coarse, sw, sh, imagescale, d_out, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e == hipSuccess) e = hipMemcpy(out, d_out, sizeof(float) * P, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = d2h(out, d_out, sizeof(float) * P);
     dfree(d_ref); dfree(d_coarse); dfree(d_out);
     if (e != hipSuccess) return fail(c, ACMMP_ERR_HIP, std::string("jbu: ") + hipGetErrorString(e));
     return ACMMP_OK;
@@ -1417,7 +1417,7 @@ static acmmp_status debug_eval(acmmp_ctx* c, int which, int n, const int* px, co
           : which == 3 ? launch_debug_ref(kp, n, dx, dy, dp, dout, c->stream)
                        : launch_debug(kp, which, n, dx, dy, dp, dout, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(float) * nout, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = d2h(out, dout, sizeof(float) * nout);
     dfree(dx); dfree(dy); dfree(dp); dfree(dout);
     if (e != hipSuccess) return fail(c, ACMMP_ERR_HIP, std::string("debug: ") + hipGetErrorString(e));
     return ACMMP_OK;

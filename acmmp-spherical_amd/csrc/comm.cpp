@@ -61,7 +61,7 @@ acmmp_status acmmp_memcpy(int device, void* dst, const void* src, size_t bytes, 
     static const hipMemcpyKind kinds[3] = {hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice};
     if (kind < 0 || kind > 2) return ACMMP_ERR_INVALID_ARGUMENT;
     TRY_HIP(hipSetDevice(device));
-    TRY_HIP(hipMemcpy(dst, src, bytes, kinds[kind]));
+    TRY_HIP(kind == 1 ? acmmp::d2h(dst, src, bytes) : hipMemcpy(dst, src, bytes, kinds[kind]));
     return ACMMP_OK;
 }
 

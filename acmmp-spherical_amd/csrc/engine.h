@@ -221,4 +221,19 @@ hipError_t launch_to_f16_pairs(const float* src, int W, int H, uint32_t* dst, in
 hipError_t launch_pad_image(const float* src, size_t pitch_floats, int W, int H, float* dst, int dst_pitch,
                             hipStream_t s);
 
+// Synchronous D2H into pageable caller memory.  Into destination pages that are not resident hipMemcpy
+// crawled: 0.32 GB/s for a 800x600 view's planes + costs (30 ms) in heap memory freed and reused, against
+// 14-50 GB/s into the same bytes once resident (profiles/r05_d2h_probe.json).  One store per 4 KiB page
+// faults them in on the CPU first; the stores write bytes the copy overwrites.  (Heap pages never touched
+// before stay slow to fault either way -- the Python binding gives large download arrays hugepage mappings of
+// their own, capi.host_empty.)
+inline hipError_t d2h(void* dst, const void* src, size_t bytes) {
+    if (bytes >= (static_cast<size_t>(256) << 10)) {
+        volatile unsigned char* p = static_cast<volatile unsigned char*>(dst);
+        for (size_t o = 0; o < bytes; o += 4096) p[o] = 0;
+        p[bytes - 1] = 0;
+    }
+    return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+}
+
 }  // namespace acmmp

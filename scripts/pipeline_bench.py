@@ -66,6 +66,8 @@ def main():
                       "total_s": round(total, 3), "s_per_view_pass": round(total / (a.views * len(pipe.passes)), 4),
                       "pass_s": [round(t, 3) for _, t in times[1:]] + [round(time.perf_counter() - last[0], 3)],
                       "stages_s": {k: round(v, 3) for k, v in sorted(pipe.stage_s.items())},
+                      "pass_compute_s": [round(p.compute_s, 3) for p in pipe.passes],
+                      "pass_stages_s": [{k: round(v, 3) for k, v in sorted(p.stages.items())} for p in pipe.passes],
                       "ref_view_frac_within_1pct_gt": acc}), flush=True)
 
 
