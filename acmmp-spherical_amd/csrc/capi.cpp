@@ -980,6 +980,7 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     // b % kNbFixRegions equal) room for every entry its blocks can queue, kNbPix x 8 hypotheses x the
     // launch's views each -- so none is ever dropped (metric 193 MB, C3 656 MB)
     kp.nb_chunk = nb_view_chunk(kp);
+    kp.nb_tile = nb_tile_order(kp);
     // the queue's key holds the colour-grid pixel in 24 bits: a larger grid (views of 8192x4096 and up) has no
     // queue, and then k_eval_nb does not interpolate (ncc_chunk interpolates only with somewhere to put its
     // fallbacks).  ACMMP_NBFIX_MAX_PC lowers the limit (a test forces that branch at a small size).
@@ -987,7 +988,7 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     if (const char* e = std::getenv("ACMMP_NBFIX_MAX_PC")) fix_max_pc = std::min<size_t>(fix_max_pc, std::strtoull(e, nullptr, 10));
     const bool fixq = c->model == kSphere && c->math == ACMMP_MATH_FAST && c->tex16 && kp.interp && Pc < fix_max_pc;
     if (!fixq && c->model == kSphere && c->math == ACMMP_MATH_FAST && c->tex16 && kp.interp && Pc >= fix_max_pc) kp.interp = 0;
-    const size_t nb_blocks = (static_cast<size_t>(Pc) + kNbPix - 1) / kNbPix;
+    const size_t nb_blocks = static_cast<size_t>(nb_block_count(kp.rows, kp.Wh, kp.nb_tile));
     const size_t fix_cap = fixq ? (nb_blocks + kNbFixRegions - 1) / kNbFixRegions * kNbPix * 8 * static_cast<size_t>(kp.nb_chunk) : 0;
     // half-sweep scratch slab: carve the pieces of engine.h's KParams out of one allocation
     size_t off[18];

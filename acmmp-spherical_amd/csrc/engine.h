@@ -132,6 +132,7 @@ struct KParams {
     unsigned long long* work;       // [256] k_eval_nb pixels with NCC work (SPHERE patch sum >= 1e-6), per block % 256
     uint32_t nb_views;              // k_eval_nb: the source views this launch evaluates (all, or a chunk of them)
     int nb_chunk;                   // views per k_eval_nb launch (nb_view_chunk)
+    int nb_tile;                    // k_eval_nb blocks as 8 x 4 tiles of the colour grid (nb_tile_order)
     int nb_count_work;              // k_eval_nb: this launch adds to `work` (the first launch of a half-sweep)
     long long Pc;                   // H * Wh
     // split refinement: k_eval_ref evaluates views [0, ref_split) of every candidate,
@@ -206,6 +207,11 @@ hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int s
                       float* out, hipStream_t s);
 // k_eval_nb's source views per launch (kernels.hip, r02 view chunking)
 int nb_view_chunk(const KParams& kp);
+int nb_tile_order(const KParams& kp);
+// k_eval_nb's block count over colour-grid rows [0, rows) of width Wh: 32-pixel row runs, or 8 x 4 tiles
+inline long long nb_block_count(long long rows, long long Wh, int tile) {
+    return tile ? ((rows + 3) / 4) * ((Wh + 7) / 8) : (rows * Wh + 31) / 32;
+}
 hipError_t launch_debug(const KParams& kp, int which, int n, const int* px, const int* py, const float4* planes,
                         float* out, hipStream_t s);
 // k_eval_nb's NCC instance on n pixels x 8 planes (planes[q * 8 + h]): out[(q * 8 + h) * V + v]

@@ -1868,9 +1868,18 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_SPH_WAVES : 
     // 8 lanes per pixel, one per neighbour direction (a pixel-major map -- a wave = 32 pixels x 2
     // directions -- measured 3% slower, profiles/r03_eval_nb_ab.txt)
     const int lp = t / kNbLanes, h = t - lp * kNbLanes;
-    const long long q = static_cast<long long>(blockIdx.x) * kNbPix + lp;
+    // the block's 32 pixels: a run of one colour-grid row, or (nb_tile) an 8 x 4 tile, a wave per tile row --
+    // either way a wave's 8 pixels are consecutive in the grid (wrow, wcol + 0..7)
+    long long wrow = 0, wcol = 0;
+    if (kp.nb_tile) {
+        const int tpr = (kp.Wh + 7) >> 3;
+        const int tr = static_cast<int>(blockIdx.x) / tpr;
+        wrow = tr * 4 + (t >> 6);
+        wcol = (static_cast<int>(blockIdx.x) - tr * tpr) * 8;
+    }
+    const long long q = kp.nb_tile ? wrow * kp.Wh + wcol + (lp & 7) : static_cast<long long>(blockIdx.x) * kNbPix + lp;
     int px = 0, py = 0;
-    const bool valid = colour_pixel(kp, colour, q, px, py);
+    const bool valid = (!kp.nb_tile || wcol + (lp & 7) < kp.Wh) && colour_pixel(kp, colour, q, px, py);
     const Patch pt = coop_patch_nb<MODEL>(kp, valid, px, py, lp, h, lds4);
     // work accounting for the roofline: pixels whose NCCs are evaluated (not short-circuited)
     const int busy = __syncthreads_count(valid && h == 0 && !(MODEL == kSphere && pt.sbw < 1e-6f));
@@ -1884,7 +1893,8 @@ __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_SPH_WAVES : 
     const uint32_t all = kp.nb_views;
     // the wave's first pixel ci = row_lo * Wh + q (colour_pixel): lane l holds pixel base + l / 8, hypothesis l % 8.
     // The output address and the fallback key are formed from it and the lane id where they are used.
-    const uint32_t wbase = static_cast<uint32_t>(uniform_int(static_cast<int>(kp.row_lo * kp.Wh + blockIdx.x * kNbPix + (t >> 6) * 8)));
+    const uint32_t wbase = static_cast<uint32_t>(uniform_int(static_cast<int>(
+        kp.nb_tile ? (kp.row_lo + wrow) * kp.Wh + wcol : kp.row_lo * kp.Wh + blockIdx.x * kNbPix + (t >> 6) * 8)));
     const uint32_t fixkey = kp.nbfix ? wbase : kFixNone;
     for_all_views_t<MODEL, nb_vb<MODEL, VB, FM>(), 3, FM ? kNbPipeFast : kNbPipeExact, TEX, FM, true>(
         kp, px, py, pt, ph, all, [&](int v, float c) {
@@ -2889,6 +2899,15 @@ int nb_view_chunk(const KParams& kp) {
     return (c <= 0 || c >= kp.V) ? kp.V : c;
 }
 
+// k_eval_nb's block shape (KParams::nb_tile): 8 x 4 tiles of the colour grid (a block's 32 pixels then span
+// 4 rows, so their patches and source footprints overlap in the CU's L1): k_eval_nb -3% at C2 (3.17 -> 3.07 ms),
+// -2.5% at C3, neutral at the metric against 32-pixel row runs (profiles/r05_ab7_ab.txt).  ACMMP_NB_TILE=0: row runs.
+int nb_tile_order(const KParams& kp) {
+    (void)kp;
+    const char* e = std::getenv("ACMMP_NB_TILE");
+    return e ? (std::atoi(e) != 0) : 1;
+}
+
 hipError_t launch_eval_nb(const KParams& kp0, int colour, hipStream_t s) {
     KParams kp = kp0;
     // interpolation fallbacks deferred to k_nb_fix: fast SPHERE with interpolated coordinates only
@@ -2995,7 +3014,8 @@ hipError_t launch_debug_nb(const KParams& kp0, int n, const int* px, const int* 
 hipError_t launch_eval_nb_views(const KParams& kp, int colour, hipStream_t s) {
     const long long npix = static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh;
     const size_t lds_nb = nb_lds_bytes(kp.model, kp.S, kp.nside);
-    const dim3 grd = static_cast<unsigned>(cdiv(npix, kNbPix));
+    const dim3 grd = static_cast<unsigned>(nb_block_count(kp.row_hi - kp.row_lo, kp.Wh, kp.nb_tile));
+    (void)npix;
     if (kp.fast) {
         if (kp.tex16) ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 1, 1><<<grd, 256, lds_nb, s>>>(kp, colour)));
         else ACMMP_DISPATCH(kp.model, kp.V, (k_eval_nb<M, VBC, 0, 1><<<grd, 256, lds_nb, s>>>(kp, colour)));
