@@ -73,3 +73,27 @@ def test_default_params_match_reference():
     assert (int(p["max_iterations"]), int(p["patch_size"]), int(p["radius_increment"]), int(p["top_k"])) == (3, 11, 2, 4)
     assert float(p["sigma_spatial"]) == 5.0 and float(p["sigma_color"]) == 3.0
     assert np.float32(p["baseline"]) == np.float32(0.54)
+
+
+def test_host_empty_download_arrays():
+    """capi.host_empty: large download arrays on 2 MiB aligned private mappings that outlive every view of them
+    and return to the pool only then; small ones plain numpy."""
+    import gc
+    small = capi.host_empty((100, 100), np.float32)
+    assert small.base is None and small.shape == (100, 100)
+    held0 = capi._POOL.held
+    a = capi.host_empty((800, 600, 4), np.float32)
+    assert a.ctypes.data % (2 << 20) == 0 and a.flags.writeable and a.flags.c_contiguous and a.dtype == np.float32
+    a[...] = 7.0
+    depth, normals = a[..., 3], a[..., :3]              # the pipeline keeps slices like these
+    ptr = a.ctypes.data
+    del a
+    gc.collect()
+    assert capi._POOL.held == held0                     # still referenced through the slices
+    assert float(depth.sum()) == 7.0 * 800 * 600 and normals.shape == (800, 600, 3)
+    del depth, normals
+    gc.collect()
+    assert capi._POOL.held > held0                      # back in the pool ...
+    b = capi.host_empty((800, 600, 4), np.float32)
+    assert b.ctypes.data == ptr                         # ... and reused by the next array of that size
+    assert capi.host_empty((600, 800), np.uint32).dtype == np.uint32
