@@ -66,9 +66,19 @@ if __name__ == "__main__":
                               "hbm_bytes_per_launch": (2.0 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0,
                               "dispatches": v["_dispatches"]}
                 for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
-                          "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "TCC_HIT", "TCC_MISS"):
+                          "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "TCC_HIT", "TCC_MISS",
+                          "TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "TCP_TCC_READ_REQ_LATENCY_sum",
+                          "TCP_PENDING_STALL_CYCLES_sum"):
                     if c in v:
                         kernels[k][c] = v[c]
+                # SURVEY.md §8d's secondary gather roof: the L1 (TCP) hit rate -- the share of TCP accesses that
+                # did not become an L2 read request -- and the mean L2 read latency the TCP saw
+                if v.get("TCP_TOTAL_CACHE_ACCESSES_sum") and "TCP_TCC_READ_REQ_sum" in v:
+                    kernels[k]["l1_hit_rate"] = 1.0 - v["TCP_TCC_READ_REQ_sum"] / v["TCP_TOTAL_CACHE_ACCESSES_sum"]
+                if v.get("TCP_TCC_READ_REQ_sum") and "TCP_TCC_READ_REQ_LATENCY_sum" in v:
+                    kernels[k]["l2_read_latency_cycles"] = v["TCP_TCC_READ_REQ_LATENCY_sum"] / v["TCP_TCC_READ_REQ_sum"]
+                if "TCC_HIT" in v and "TCC_MISS" in v and v["TCC_HIT"] + v["TCC_MISS"] > 0:
+                    kernels[k]["l2_hit_rate"] = v["TCC_HIT"] / (v["TCC_HIT"] + v["TCC_MISS"])
         json.dump({"config": {"width": a.width, "height": a.height, "n_src": a.n_src, "model": a.model, "math": a.math},
                    "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 bytes per dispatch (gfx950 FETCH_SIZE counts 1/2)",
                    "kernels": kernels}, open(a.json, "w"), indent=1)
