@@ -1588,12 +1588,16 @@ __global__ __launch_bounds__(256) void k_init(const KParams kp) {
 // kernel-entry snapshot: neighbour planes/costs come from the colour's current buffer, the result
 // goes to its other buffer.
 
+// (the colour's buffer chosen by a select between the two kernel-argument pointers: indexed by the lane's parity,
+// the pointer itself was loaded from the argument block first -- a second dependent round trip per access)
 __device__ __forceinline__ float cost_at(const KParams& kp, int x, int y) {
-    return kp.cost_cs[(x + y) & 1][cs_index(kp, x, y)];
+    const float* b = ((x + y) & 1) ? kp.cost_cs[1] : kp.cost_cs[0];
+    return b[cs_index(kp, x, y)];
 }
 __device__ __forceinline__ float4 plane_at(const KParams& kp, int pos) {
     const int x = pos & 0xFFFF, y = pos >> 16;
-    return kp.plane_cs[(x + y) & 1][cs_index(kp, x, y)];
+    const float4* b = ((x + y) & 1) ? kp.plane_cs[1] : kp.plane_cs[0];
+    return b[cs_index(kp, x, y)];
 }
 __device__ __forceinline__ int packpos(int x, int y) { return x | (y << 16); }
 
@@ -2005,12 +2009,14 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
         flag[d] = pos[d] >= 0;
     }
     // cost_array[8][32] = {2.0f}: unavailable directions read as 0, element [0][0] as 2 (:957)
+    // (the load is unconditional and the value selected after it: a load behind the flag's branch was waited for
+    // before the next one issued -- 128 serial L2 / HBM round trips per pixel at V = 15; every slab entry exists)
     auto cost_arr = [&](int d, int v) -> float {
         bool f = flag[0];
 #pragma unroll
         for (int k = 1; k < 8; ++k) if (k == d) f = flag[k];
-        if (!f) return (d == 0 && v == 0) ? 2.0f : 0.0f;
-        return kp.hyp_cost[(static_cast<long long>(d) * V + v) * Pc + ci];
+        const float raw = kp.hyp_cost[(static_cast<long long>(d) * V + v) * Pc + ci];
+        return f ? raw : ((d == 0 && v == 0) ? 2.0f : 0.0f);
     };
 
     // ---- joint view selection :1146-1208
@@ -2040,7 +2046,8 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (flag[2 * i]) {
-                const uint32_t sv = kp.sel_cs[(nbx[i] + nby[i]) & 1][cs_index(kp, nbx[i], nby[i])];
+                const uint32_t* sb = ((nbx[i] + nby[i]) & 1) ? kp.sel_cs[1] : kp.sel_cs[0];
+                const uint32_t sv = sb[cs_index(kp, nbx[i], nby[i])];
 #pragma unroll
                 for (int j = 0; j < VMAX; ++j)
                     if (j < V) vsp[j] += ((sv >> j) & 1u) ? 0.9f : 0.1f;
@@ -2050,6 +2057,13 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
     const float cost_threshold = static_cast<float>(0.8 * static_cast<double>(
         det_exp(static_cast<float>(iter * iter) / (-90.0f))));
     float probs[VMAX];
+    // (wide launches: the next view's 8 costs are loaded before this view's are used, so one view's loads are in
+    // flight while the previous view computes)
+    float nxt[kRegCost ? 1 : 8];
+    if constexpr (!kRegCost) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) nxt[j] = cost_arr(j, 0);
+    }
 #pragma unroll
     for (int i = 0; i < VMAX; i++) {
         probs[i] = 0.0f;
@@ -2057,11 +2071,34 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
         float count = 0.0f;
         int count_false = 0;
         float tmpw = 0.0f;
+        if constexpr (kRegCost) {
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const float c = cost_at_dv(j, i);
-            if (c < cost_threshold) { tmpw += det_exp(c * c / (-0.18f)); count++; }
-            if (c > 1.2f) count_false++;
+            for (int j = 0; j < 8; j++) {
+                const float c = cost_at_dv(j, i);
+                if (c < cost_threshold) { tmpw += det_exp(c * c / (-0.18f)); count++; }
+                if (c > 1.2f) count_false++;
+            }
+        } else {
+            // branch-free over the 8 directions (the exponential taken for every cost, added only below the
+            // threshold: + 0.0f leaves the non-negative sum's bits as they are): no branch between the loads, so
+            // they issue together instead of one L2 / HBM round trip each (k_select waited on memory for 73% of
+            // its wave cycles at C3)
+            float cs[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) cs[j] = nxt[j];
+            if (i + 1 < V) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) nxt[j] = cost_arr(j, i + 1);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const float c = cs[j];
+                const bool lt = c < cost_threshold;
+                const float e = det_exp(c * c / (-0.18f));
+                tmpw += lt ? e : 0.0f;
+                count += lt ? 1.0f : 0.0f;
+                count_false += c > 1.2f ? 1 : 0;
+            }
         }
         float pr = 0.0f;
         if (count > 2 && count_false < 3) pr = tmpw / count;
@@ -2122,9 +2159,25 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
                 if (j < V) add_view(j, ca[i][j]);
         } else {
             // only the selected views' costs are read (a zero-weight view adds nothing): at V = 15 about
-            // a quarter of the 8 x V matrix, which k_eval_nb's slab holds in HBM at C3 sizes
-            for (int j = 0; j < V; ++j)
-                if ((temp_sel >> j) & 1u) add_view(j, cost_arr(i, j));
+            // a quarter of the 8 x V matrix, which k_eval_nb's slab holds in HBM at C3 sizes.  Branch-free: an
+            // unselected view loads the pixel's own first entry (cached) and adds nothing, so the loads issue
+            // together
+            const bool fi = flag[i];
+            if (GEOM || VMAX > 16) {                         // (at 32 views the unrolled form spilled 29 dwords)
+                for (int j = 0; j < V; ++j)
+                    if ((temp_sel >> j) & 1u) add_view(j, cost_arr(i, j));
+            } else {
+                // branch-free, views beyond V included as never taken (temp_sel has no bit there): one basic block,
+                // so the loads issue together.  (take <=> weight > 0: add_view's own test, as a select)
+#pragma unroll
+                for (int j = 0; j < VMAX; ++j) {
+                    const bool take = (temp_sel >> j) & 1u;
+                    const float raw = kp.hyp_cost[take ? (static_cast<long long>(i) * V + j) * Pc + ci : ci];
+                    const float c = fi ? raw : ((i == 0 && j == 0) ? 2.0f : 0.0f);
+                    const float nf = fmaf(vw_get(vwp, j), c, fc);
+                    fc = take ? nf : fc;
+                }
+            }
         }
         final_costs[i] = fc / weight_norm;
     }
@@ -2142,21 +2195,38 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
     // (a candidate whose wave skipped a view) are evaluated here; that is rare and only for them.
     float* cvec = kp.cvec[colour] + ci;
     uint32_t miss = 0u;
-    for (int v = 0; v < V; ++v)
-        if (vw_get(vwp, v) > 0.0f && cvec[v * Pc] != cvec[v * Pc]) miss |= 1u << v;
+    float cost_now = 0.0f;
+    constexpr bool kCvecLoop = GEOM || VMAX > 16;
+    if (kCvecLoop) {
+        for (int v = 0; v < V; ++v)
+            if (vw_get(vwp, v) > 0.0f && cvec[v * Pc] != cvec[v * Pc]) miss |= 1u << v;
+    } else {
+        // branch-free: the selected views' cached costs loaded together (an unselected or absent view reads the
+        // first entry, cached, and is not used), folded in view order as below unless one is missing
+#pragma unroll
+        for (int v = 0; v < VMAX; ++v) {
+            const bool take = (temp_sel >> v) & 1u;
+            const float c = cvec[take ? static_cast<long long>(v) * Pc : 0];
+            miss |= (take && c != c) ? (1u << v) : 0u;
+            const float nc = fmaf(vw_get(vwp, v), c, cost_now);
+            cost_now = take ? nc : cost_now;
+        }
+    }
     if (miss) {
         const Patch pt = make_patch<MODEL>(kp, px, py);
         for_all_views<MODEL, 1, 0, true>(kp, px, py, pt, cur_plane, wave_or(miss, V), [&](int v, float c) {
             if ((miss >> v) & 1u) cvec[v * Pc] = c;
         });
     }
-    float cost_now = 0.0f;
-    for (int v = 0; v < V; ++v) {
-        const float w = vw_get(vwp, v);
-        if (w > 0.0f) {
-            const float c = cvec[v * Pc];
-            if (GEOM) cost_now = fmaf(w, fmaf(0.2f, geom_cost<MODEL>(kp, v + 1, cur_plane, px, py, dc), c), cost_now);
-            else cost_now = fmaf(w, c, cost_now);
+    if (kCvecLoop || miss) {
+        cost_now = 0.0f;
+        for (int v = 0; v < V; ++v) {
+            const float w = vw_get(vwp, v);
+            if (w > 0.0f) {
+                const float c = cvec[v * Pc];
+                if (GEOM) cost_now = fmaf(w, fmaf(0.2f, geom_cost<MODEL>(kp, v + 1, cur_plane, px, py, dc), c), cost_now);
+                else cost_now = fmaf(w, c, cost_now);
+            }
         }
     }
     cost_now /= weight_norm;
