@@ -1604,96 +1604,93 @@ __device__ __forceinline__ int packpos(int x, int y) { return x | (y << 16); }
 // Adaptive checkerboard sampling of one direction (ACMMP.cu:965-1143); returns the packed position
 // or -1 when the direction is unavailable (flag[d] == false).
 __device__ __forceinline__ int pick_neighbour(const KParams& kp, int d, int px, int py) {
+    // Branch-free: every candidate's cost is loaded (an out-of-image one from the first candidate's position, not
+    // taken) and the strict-< scan in the reference's order runs on selects -- behind the bounds branches each
+    // load was waited for before the next issued (k_pick: 7-11 serial round trips per pixel)
     const int width = kp.W, height = kp.H;
     float cmin;
     int cpos;
+    auto take = [&](bool ok, int x, int y) {
+        const float c = cost_at(kp, x, y);
+        const bool better = ok && c < cmin;
+        cmin = better ? c : cmin;
+        cpos = better ? packpos(x, y) : cpos;
+    };
     switch (d) {
     case 1:                                                   // up_far
         if (!(py > 2)) return -1;
         cmin = cost_at(kp, px, py - 3); cpos = packpos(px, py - 3);
-        for (int i = 1; i < 11; ++i) if (py > 2 + 2 * i) {
-            const float c = cost_at(kp, px, py - 3 - 2 * i);
-            if (c < cmin) { cmin = c; cpos = packpos(px, py - 3 - 2 * i); }
+#pragma unroll
+        for (int i = 1; i < 11; ++i) {
+            const bool ok = py > 2 + 2 * i;
+            take(ok, px, ok ? py - 3 - 2 * i : py - 3);
         }
         return cpos;
     case 3:                                                   // down_far
         if (!(py < height - 3)) return -1;
         cmin = cost_at(kp, px, py + 3); cpos = packpos(px, py + 3);
-        for (int i = 1; i < 11; ++i) if (py < height - 3 - 2 * i) {
-            const float c = cost_at(kp, px, py + 3 + 2 * i);
-            if (c < cmin) { cmin = c; cpos = packpos(px, py + 3 + 2 * i); }
+#pragma unroll
+        for (int i = 1; i < 11; ++i) {
+            const bool ok = py < height - 3 - 2 * i;
+            take(ok, px, ok ? py + 3 + 2 * i : py + 3);
         }
         return cpos;
     case 5:                                                   // left_far
         if (!(px > 2)) return -1;
         cmin = cost_at(kp, px - 3, py); cpos = packpos(px - 3, py);
-        for (int i = 1; i < 11; ++i) if (px > 2 + 2 * i) {
-            const float c = cost_at(kp, px - 3 - 2 * i, py);
-            if (c < cmin) { cmin = c; cpos = packpos(px - 3 - 2 * i, py); }
+#pragma unroll
+        for (int i = 1; i < 11; ++i) {
+            const bool ok = px > 2 + 2 * i;
+            take(ok, ok ? px - 3 - 2 * i : px - 3, py);
         }
         return cpos;
     case 7:                                                   // right_far
         if (!(px < width - 3)) return -1;
         cmin = cost_at(kp, px + 3, py); cpos = packpos(px + 3, py);
-        for (int i = 1; i < 11; ++i) if (px < width - 3 - 2 * i) {
-            const float c = cost_at(kp, px + 3 + 2 * i, py);
-            if (c < cmin) { cmin = c; cpos = packpos(px + 3 + 2 * i, py); }
+#pragma unroll
+        for (int i = 1; i < 11; ++i) {
+            const bool ok = px < width - 3 - 2 * i;
+            take(ok, ok ? px + 3 + 2 * i : px + 3, py);
         }
         return cpos;
     case 0:                                                   // up_near (V shape, same colour)
         if (!(py > 0)) return -1;
         cmin = cost_at(kp, px, py - 1); cpos = packpos(px, py - 1);
+#pragma unroll
         for (int i = 0; i < 3; ++i) {
-            if (py > 1 + i && px > i) {
-                const float c = cost_at(kp, px - i, py - 2 - i);
-                if (c < cmin) { cmin = c; cpos = packpos(px - i, py - 2 - i); }
-            }
-            if (py > 1 + i && px < width - 1 - i) {
-                const float c = cost_at(kp, px + i, py - 2 - i);
-                if (c < cmin) { cmin = c; cpos = packpos(px + i, py - 2 - i); }
-            }
+            const bool a = py > 1 + i && px > i, b = py > 1 + i && px < width - 1 - i;
+            take(a, a ? px - i : px, a ? py - 2 - i : py - 1);
+            take(b, b ? px + i : px, b ? py - 2 - i : py - 1);
         }
         return cpos;
     case 2:                                                   // down_near
         if (!(py < height - 1)) return -1;
         cmin = cost_at(kp, px, py + 1); cpos = packpos(px, py + 1);
+#pragma unroll
         for (int i = 0; i < 3; ++i) {
-            if (py < height - 2 - i && px > i) {
-                const float c = cost_at(kp, px - i, py + 2 + i);
-                if (c < cmin) { cmin = c; cpos = packpos(px - i, py + 2 + i); }
-            }
-            if (py < height - 2 - i && px < width - 1 - i) {
-                const float c = cost_at(kp, px + i, py + 2 + i);
-                if (c < cmin) { cmin = c; cpos = packpos(px + i, py + 2 + i); }
-            }
+            const bool a = py < height - 2 - i && px > i, b = py < height - 2 - i && px < width - 1 - i;
+            take(a, a ? px - i : px, a ? py + 2 + i : py + 1);
+            take(b, b ? px + i : px, b ? py + 2 + i : py + 1);
         }
         return cpos;
     case 4:                                                   // left_near
         if (!(px > 0)) return -1;
         cmin = cost_at(kp, px - 1, py); cpos = packpos(px - 1, py);
+#pragma unroll
         for (int i = 0; i < 3; ++i) {
-            if (px > 1 + i && py > i) {
-                const float c = cost_at(kp, px - 2 - i, py - i);
-                if (c < cmin) { cmin = c; cpos = packpos(px - 2 - i, py - i); }
-            }
-            if (px > 1 + i && py < height - 1 - i) {
-                const float c = cost_at(kp, px - 2 - i, py + i);
-                if (c < cmin) { cmin = c; cpos = packpos(px - 2 - i, py + i); }
-            }
+            const bool a = px > 1 + i && py > i, b = px > 1 + i && py < height - 1 - i;
+            take(a, a ? px - 2 - i : px - 1, a ? py - i : py);
+            take(b, b ? px - 2 - i : px - 1, b ? py + i : py);
         }
         return cpos;
     default:                                                  // 6: right_near
         if (!(px < width - 1)) return -1;
         cmin = cost_at(kp, px + 1, py); cpos = packpos(px + 1, py);
+#pragma unroll
         for (int i = 0; i < 3; ++i) {
-            if (px < width - 2 - i && py > i) {
-                const float c = cost_at(kp, px + 2 + i, py - i);
-                if (c < cmin) { cmin = c; cpos = packpos(px + 2 + i, py - i); }
-            }
-            if (px < width - 2 - i && py < height - 1 - i) {
-                const float c = cost_at(kp, px + 2 + i, py + i);
-                if (c < cmin) { cmin = c; cpos = packpos(px + 2 + i, py + i); }
-            }
+            const bool a = px < width - 2 - i && py > i, b = px < width - 2 - i && py < height - 1 - i;
+            take(a, a ? px + 2 + i : px + 1, a ? py - i : py);
+            take(b, b ? px + 2 + i : px + 1, b ? py + i : py);
         }
         return cpos;
     }
