@@ -2276,12 +2276,17 @@ __global__ __launch_bounds__(256, 5) void k_select(const KParams kp, const int c
         const float depth_prior = depth_from_plane(prior, dc);
         const float beta = 0.18f;
         if (use_prior) {
+            // the 8 neighbour planes loaded before any of them is tested (an unavailable direction reads this
+            // pixel's own plane, unused): behind `flag[i]` each load was waited for before the next
+            float4 nbs[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) nbs[i] = plane_at(kp, flag[i] ? pos[i] : packpos(px, py));
             float rfc[8];
 #pragma unroll
             for (int i = 0; i < 8; i++) {
                 rfc[i] = 0.0f;
                 if (flag[i]) {
-                    const float4 nb = plane_at(kp, pos[i]);
+                    const float4 nb = nbs[i];
                     const float ddiff = depth_from_plane(nb, dc) - depth_prior;
                     const float ad = det_acos(dot3n(prior, nb));
                     const float pr = fmaf(det_exp((-ddiff) * ddiff / two_dss), det_exp((-ad) * ad / two_ass), gamma);
