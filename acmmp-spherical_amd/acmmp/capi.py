@@ -93,7 +93,7 @@ EXPORTS = [
     "acmmp_band_copy_rows", "acmmp_band_get_rows", "acmmp_band_set_rows", "acmmp_band_end",
     "acmmp_fusion_create", "acmmp_fusion_set_view", "acmmp_fusion_run", "acmmp_fusion_last_error",
     "acmmp_fusion_destroy", "acmmp_image_cache_create", "acmmp_image_cache_destroy", "acmmp_image_cache_stats",
-    "acmmp_upload_views_keyed",
+    "acmmp_upload_views_keyed", "acmmp_device_checksum", "acmmp_device_identity", "acmmp_clock_probe",
 ]
 
 
@@ -187,6 +187,9 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_image_cache_destroy.argtypes = [vp]
     L.acmmp_image_cache_stats.argtypes = [vp, vp]
     L.acmmp_upload_views_keyed.argtypes = [vp, vp, i32, vp, vp, vp, vp, i32]
+    L.acmmp_device_checksum.argtypes = [i32, vp, C.c_size_t, vp]
+    L.acmmp_device_identity.argtypes = [i32, vp, i32, vp]
+    L.acmmp_clock_probe.argtypes = [i32, C.c_float, vp]
     for name in EXPORTS:
         fn = getattr(L, name)
         if name not in ("acmmp_destroy", "acmmp_status_str", "acmmp_last_error", "acmmp_abi_version", "acmmp_device_count",
@@ -207,6 +210,54 @@ def device_count() -> int:
 
 def _p(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def checksum_host(arr) -> int:
+    """acmmp_device_checksum on a host array (its bytes as little-endian 32-bit words): the sum mod 2^64 of
+    splitmix64's finaliser of (i << 32) | w_i.  The CPU side of the exchange check and its tests."""
+    w = np.frombuffer(np.ascontiguousarray(arr).tobytes(), np.uint32).astype(np.uint64)
+    z = (np.arange(w.size, dtype=np.uint64) << np.uint64(32)) | w
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+        z = z ^ (z >> np.uint64(31))
+        return int(np.sum(z, dtype=np.uint64))
+
+
+def device_identity(device: int) -> dict:
+    """PCI bus id, UUID and (where the KFD topology lists the device) its KFD unique_id: which physical GPU a
+    measurement ran on (bench.py `device`)."""
+    L = load_library()
+    bus = C.create_string_buffer(64)
+    uuid = np.zeros(16, np.uint8)
+    _host_check(L.acmmp_device_identity(device, C.cast(bus, C.c_void_p), 64, _p(uuid)), "device_identity")
+    pci = bus.value.decode()
+    out = {"pci_bus_id": pci, "uuid": uuid.tobytes().hex(), "kfd_unique_id": None}
+    try:                                        # KFD node whose location_id is this bus:device.function
+        dom, bus_, devfn = pci.split(":")
+        dev_, fn = devfn.split(".")
+        loc = (int(bus_, 16) << 8) | (int(dev_, 16) << 3) | int(fn, 16)
+        root = "/sys/class/kfd/kfd/topology/nodes"
+        for node in sorted(os.listdir(root)):
+            with open(os.path.join(root, node, "properties")) as fh:
+                props = dict(ln.split(None, 1) for ln in fh if len(ln.split(None, 1)) == 2)
+            if (int(props.get("location_id", "-1")) == loc and
+                    int(props.get("domain", "0")) == int(dom, 16)):
+                out["kfd_unique_id"] = props.get("unique_id", "").strip() or None
+                out["kfd_node"] = int(node)
+                break
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def clock_probe(device: int, warm_ms: float = 1500.0) -> dict:
+    """acmmp_clock_probe: the shader clock held under a VALU-dense load (median / min / max GHz over
+    workgroups) after warm_ms of back-to-back launches."""
+    out = np.zeros(4, np.float64)
+    _host_check(load_library().acmmp_clock_probe(device, float(warm_ms), _p(out)), "clock_probe")
+    return {"ghz": round(float(out[0]), 4), "ghz_min": round(float(out[1]), 4), "ghz_max": round(float(out[2]), 4),
+            "probe_launch_ms": round(float(out[3]), 3), "warm_ms": warm_ms}
 
 
 class ImageCache:
@@ -681,6 +732,13 @@ class DeviceBuffer:
         a = host_empty(self.shape, np.float32)
         _host_check(self.L.acmmp_memcpy(self.device, _p(a), C.c_void_p(self.ptr), self.nbytes, 1), "memcpy D2H")
         return a
+
+    def checksum(self) -> int:
+        """acmmp_device_checksum of the buffer (equal to checksum_host of its download)."""
+        out = C.c_uint64(0)
+        _host_check(self.L.acmmp_device_checksum(self.device, C.c_void_p(self.ptr), self.nbytes, C.byref(out)),
+                    "device_checksum")
+        return int(out.value)
 
     def free(self):
         if self.ptr:

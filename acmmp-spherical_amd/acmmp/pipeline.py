@@ -243,20 +243,61 @@ class LocalExchange:
         pass
 
 
+class ExchangeMismatch(RuntimeError):
+    """A map some rank holds after the depth exchange differs from its owner's."""
+
+
+def mismatched_maps(comm, checksums) -> list:
+    """Indices of the maps whose checksum is not the same on every rank of `comm` (one allreduce-max over
+    the 32-bit halves and their negations: max == min on every rank iff all ranks agree).  Each map's owner
+    passes the checksum it took BEFORE the broadcast and every other rank the one of what it received, so
+    agreement means every rank holds the owner's bytes (a broadcast from the wrong root overwrites the owner's
+    buffer too, so post-broadcast checksums alone would agree on the wrong map).  comm: anything with
+    allreduce_max(float64 array) -> array."""
+    c = np.asarray(checksums, np.uint64)
+    n = c.size
+    if n == 0:
+        return []
+    hi = (c >> np.uint64(32)).astype(np.float64)
+    lo = (c & np.uint64(0xFFFFFFFF)).astype(np.float64)
+    m = np.asarray(comm.allreduce_max(np.concatenate([hi, lo, -hi, -lo])), np.float64)
+    return [i for i in range(n) if m[i] != -m[2 * n + i] or m[n + i] != -m[3 * n + i]]
+
+
 class RcclExchange:
     """Depth maps live in HBM (DeviceBuffer per (key, view)); a pass's outputs are broadcast from
-    their owners with one grouped RCCL call."""
+    their owners with one grouped RCCL call.  verify (default on; ACMMP_VERIFY_EXCHANGE=0 turns it off):
+    after the broadcast every rank checksums each map it now holds (acmmp_device_checksum, in HBM) and the
+    ranks compare them (mismatched_maps), so a wrong root, buffer or ordering stops the run."""
 
-    def __init__(self, comm: capi.Comm, device: int):
+    def __init__(self, comm: capi.Comm, device: int, verify: bool | None = None):
         self.comm, self.device = comm, device
         self.world, self.rank = comm.nranks, comm.rank
+        self.verify = os.environ.get("ACMMP_VERIFY_EXCHANGE", "1") != "0" if verify is None else verify
+        self.maps_verified = 0
 
     def share(self, key, views, owners, store):
         bufs = [store.device_map(key, v) for v in views]
         # the broadcast reads maps the engine contexts exported on their own streams: order it after them
-        for ctx in store.take_producers():
+        producers = store.take_producers()
+        for ctx in producers:
             self.comm.after(ctx)
+        pre = {}
+        if self.verify:
+            for ctx in producers:                    # the exports complete before the owner checksums them
+                ctx.synchronize()
+            pre = {i: bufs[i].checksum() for i, v in enumerate(views) if owners[v] == self.rank}
         self.comm.broadcast(bufs, [owners[v] for v in views])
+        if self.verify:
+            post = [b.checksum() for b in bufs]
+            # an owner whose own buffer changed in the broadcast reports the complement of its checksum
+            sums = [post[i] if i not in pre else (pre[i] if post[i] == pre[i] else pre[i] ^ ((1 << 64) - 1))
+                    for i in range(len(bufs))]
+            bad = mismatched_maps(self.comm, sums)
+            if bad:
+                raise ExchangeMismatch(f"depth exchange of {key}: views {[views[i] for i in bad]} differ "
+                                       f"between ranks after the broadcast")
+            self.maps_verified += len(bufs)
         for v in views:
             if owners[v] != self.rank:
                 store.host.pop((key, v), None)      # re-read from HBM on demand

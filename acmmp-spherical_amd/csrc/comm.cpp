@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -62,6 +63,94 @@ acmmp_status acmmp_memcpy(int device, void* dst, const void* src, size_t bytes, 
     if (kind < 0 || kind > 2) return ACMMP_ERR_INVALID_ARGUMENT;
     TRY_HIP(hipSetDevice(device));
     TRY_HIP(kind == 1 ? acmmp::d2h(dst, src, bytes) : hipMemcpy(dst, src, bytes, kinds[kind]));
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_device_checksum(int device, const void* ptr, size_t bytes, uint64_t* out) {
+    if (!out || (!ptr && bytes) || bytes % 4) return ACMMP_ERR_INVALID_ARGUMENT;
+    *out = 0;
+    if (!bytes) return ACMMP_OK;
+    TRY_HIP(hipSetDevice(device));
+    unsigned long long* d = nullptr;
+    TRY_HIP(hipMalloc(&d, sizeof(*d)));
+    unsigned long long h = 0;
+    hipError_t e = hipMemsetAsync(d, 0, sizeof(*d), nullptr);
+    if (e == hipSuccess) e = acmmp::launch_checksum(ptr, bytes, d, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    TRY_HIP(e);
+    *out = h;
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_device_identity(int device, char* pci_bus_id, int len, uint8_t uuid[16]) {
+    if (!pci_bus_id || len < 16 || !uuid) return ACMMP_ERR_INVALID_ARGUMENT;
+    TRY_HIP(hipDeviceGetPCIBusId(pci_bus_id, len, device));
+    hipDevice_t dv;
+    TRY_HIP(hipDeviceGet(&dv, device));
+    hipUUID u;
+    TRY_HIP(hipDeviceGetUuid(&u, dv));
+    std::memcpy(uuid, u.bytes, 16);
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_clock_probe(int device, float warm_ms, double out[4]) {
+    if (!out) return ACMMP_ERR_INVALID_ARGUMENT;
+    TRY_HIP(hipSetDevice(device));
+    int cus = 0;
+    TRY_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    const int blocks = std::max(1, cus) * 16;            // 4 waves of 256 lanes per block: 16 per SIMD
+    std::vector<float> rnd(65536);
+    uint32_t x = 0x9e3779b9u;
+    for (float& r : rnd) {                               // uniform in [-1, 1): random operands, not zeros
+        x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+        r = static_cast<float>(x >> 8) * (2.0f / 16777216.0f) - 1.0f;
+    }
+    float *d_rnd = nullptr, *d_sink = nullptr;
+    acmmp::ClockStamp* d_st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipError_t e = hipMalloc(&d_rnd, rnd.size() * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&d_sink, static_cast<size_t>(blocks) * 256 * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&d_st, static_cast<size_t>(blocks) * sizeof(acmmp::ClockStamp));
+    if (e == hipSuccess) e = hipMemcpy(d_rnd, rnd.data(), rnd.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    std::vector<acmmp::ClockStamp> st(blocks);
+    float ms = 0.f;
+    int iters = 4096;
+    // size one launch to ~5 ms, keep the chip under that load for warm_ms, then one stamped launch
+    for (int k = 0; e == hipSuccess && k < 3; ++k) {
+        e = hipEventRecord(e0, nullptr);
+        if (e == hipSuccess) e = acmmp::launch_clock_probe(d_rnd, iters, blocks, nullptr, d_sink, nullptr);
+        if (e == hipSuccess) e = hipEventRecord(e1, nullptr);
+        if (e == hipSuccess) e = hipEventSynchronize(e1);
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+        if (e == hipSuccess && ms > 0.f) iters = std::max(256, std::min(1 << 22, static_cast<int>(iters * 5.0f / ms)));
+    }
+    const int warm = std::max(0, static_cast<int>(warm_ms / 5.0f));
+    for (int k = 0; e == hipSuccess && k < warm; ++k)
+        e = acmmp::launch_clock_probe(d_rnd, iters, blocks, nullptr, d_sink, nullptr);
+    if (e == hipSuccess) e = hipEventRecord(e0, nullptr);
+    if (e == hipSuccess) e = acmmp::launch_clock_probe(d_rnd, iters, blocks, d_st, d_sink, nullptr);
+    if (e == hipSuccess) e = hipEventRecord(e1, nullptr);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e == hipSuccess) e = hipMemcpy(st.data(), d_st, st.size() * sizeof(st[0]), hipMemcpyDeviceToHost);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(d_rnd);
+    (void)hipFree(d_sink);
+    (void)hipFree(d_st);
+    TRY_HIP(e);
+    std::vector<double> ghz;
+    for (const acmmp::ClockStamp& c : st)
+        if (c.ticks > 0) ghz.push_back(static_cast<double>(c.cycles) / static_cast<double>(c.ticks) * 0.1);
+    if (ghz.empty()) return ACMMP_ERR_HIP;
+    std::sort(ghz.begin(), ghz.end());
+    out[0] = ghz[ghz.size() / 2];
+    out[1] = ghz.front();
+    out[2] = ghz.back();
+    out[3] = ms;
     return ACMMP_OK;
 }
 

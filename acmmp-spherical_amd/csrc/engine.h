@@ -205,6 +205,14 @@ hipError_t launch_export_depth(const float4* planes, long long P, float* dst, hi
 hipError_t launch_copy(const void* src, void* dst, size_t bytes, hipStream_t s);  // bytes % 4 == 0
 hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int sw, int sh, int imagescale,
                       float* out, hipStream_t s);
+// Diagnostic clock probe (acmmp_clock_probe): per workgroup, shader cycles and 100 MHz ticks around a
+// VALU-dense loop of `iters` steps on `rnd` (65536 floats); stamps may be null (warm-up launches).
+struct ClockStamp {
+    unsigned long long cycles, ticks;
+};
+hipError_t launch_clock_probe(const float* rnd, int iters, int blocks, ClockStamp* stamps, float* sink, hipStream_t s);
+// acmmp_device_checksum: adds the checksum of `bytes` (multiple of 4) at ptr to *out (device, pre-zeroed)
+hipError_t launch_checksum(const void* ptr, size_t bytes, unsigned long long* out, hipStream_t s);
 // k_eval_nb's source views per launch (kernels.hip, r02 view chunking)
 int nb_view_chunk(const KParams& kp);
 int nb_tile_order(const KParams& kp);

@@ -3553,6 +3553,89 @@ hipError_t launch_jbu(const float* ref, int W, int H, const float* coarse, int s
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ diagnostic: the shader clock under load
+//
+// Not on the PatchMatch path (acmmp_clock_probe, bench.py's `clock`).  The chip lowers its clock under load,
+// by different amounts on different devices (MI355X_MICROARCH.md "DVFS give-back" (5): 1.51-1.69 GHz across
+// devices for issue-dense bodies), and k_eval_nb is issue-dense: its time tracks that clock.  Eight independent
+// chains per lane of the logistic map x <- r x (1 - x) at r = 3.99 (a multiply and an fma per step): a
+// VALU-dense body whose operands stay chaotic, so their bits keep toggling as k_eval_nb's data does (an fma
+// chain converging to a fixed point draws less power and holds a higher clock, ibid. item 1); the first lane
+// of each workgroup reads the shader-cycle counter and the constant 100 MHz counter around the loop (ibid.
+// item 6), and the host takes the median of the per-workgroup ratios.
+__global__ __launch_bounds__(256) void k_clock_probe(const float* __restrict__ rnd, int iters, ClockStamp* stamps,
+                                                     float* __restrict__ sink) {
+    const unsigned gid = blockIdx.x * 256u + threadIdx.x;
+    float x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = 0.25f + 0.5f * fabsf(rnd[(gid * 8u + k) & 65535u]);
+    constexpr float r = 3.99f;
+    unsigned long long t0 = 0, r0 = 0;
+    if (stamps) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float t = r * x[k];
+            x[k] = fmaf(-t, x[k], t);
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += x[k];
+    if (stamps) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) {
+            ClockStamp c;
+            c.cycles = t1 - t0;
+            c.ticks = r1 - r0;
+            stamps[blockIdx.x] = c;
+        }
+    }
+    sink[gid] = s;
+}
+
+hipError_t launch_clock_probe(const float* rnd, int iters, int blocks, ClockStamp* stamps, float* sink, hipStream_t s) {
+    k_clock_probe<<<blocks, 256, 0, s>>>(rnd, iters, stamps, sink);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ exchange check: checksum of a device buffer
+//
+// sum over the buffer's 32-bit words w_i of mix64((i << 32) | w_i) mod 2^64 (acmmp_device_checksum): a word's
+// value and position both enter, and the sum does not depend on the order it is formed in.  The pipeline
+// compares every rank's checksum of each map a pass exchanged (acmmp/pipeline.py RcclExchange), so a wrong
+// root, buffer or ordering in the grouped broadcast fails the run instead of feeding a wrong map on.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_checksum(const uint32_t* __restrict__ w, long long n, unsigned long long* out) {
+    unsigned long long acc = 0;
+    for (long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x; i < n;
+         i += static_cast<long long>(gridDim.x) * 256)
+        acc += mix64((static_cast<unsigned long long>(i) << 32) | w[i]);
+    __shared__ unsigned long long part[256];
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) part[threadIdx.x] += part[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicAdd(out, part[0]);
+}
+
+hipError_t launch_checksum(const void* ptr, size_t bytes, unsigned long long* out, hipStream_t s) {
+    const long long n = static_cast<long long>(bytes / 4);
+    const unsigned grd = static_cast<unsigned>(std::max<long long>(1, std::min<long long>((n + 255) / 256, 2048)));
+    k_checksum<<<grd, 256, 0, s>>>(static_cast<const uint32_t*>(ptr), n, out);
+    return hipGetLastError();
+}
+
 #endif  // ACMMP_IN_TU(0)
 
 }  // namespace acmmp

@@ -119,6 +119,9 @@ def parse():
     ap.add_argument("--timed-only", action="store_true",
                     help="profiling: nothing runs on the GPU after the timed steps (no other math mode, latency, "
                          "PCIe, variant, end-to-end or CPU legs), so a kernel trace's last launches are the timed ones")
+    ap.add_argument("--no-clock", action="store_true", help="skip the clock probe after the timed region")
+    ap.add_argument("--clock-warm-ms", type=float, default=1500.0,
+                    help="clock probe: ms of back-to-back VALU-dense launches before the stamped one")
     ap.add_argument("--allow-shared-gpus", action="store_true",
                     help="rehearsal only: let more ranks than GPUs share devices round-robin (never a scaling point)")
     ap.add_argument("--dry-run", action="store_true",
@@ -309,9 +312,18 @@ def depth_exchange(args, ctx, rank, world, device, dist, allmax, reps=5):
         comm = capi.Comm(device, uid[0], world, rank)
         bufs = [capi.DeviceBuffer(device, (args.height, args.width)) for _ in range(world)]
         ctx.export_depth(bufs[rank])
+        ctx.synchronize()
+        own = bufs[rank].checksum()                                  # the owner's map before the broadcast
         comm.after(ctx)                                              # the broadcast waits for the export
         comm.broadcast(bufs, list(range(world)))                     # warm-up
         ok = all(np.isfinite(b.download()).mean() > 0.5 for b in bufs)
+        # every received map bit for bit against its owner's: each rank's checksum of every buffer after the
+        # broadcast (acmmp_device_checksum) and each owner's from before it, gathered over the gloo group
+        # (a wrong root / buffer / order in the grouped broadcast shows here, a wrong root included: it
+        # overwrites the owner's buffer as well)
+        got = [None] * world
+        dist.all_gather_object(got, {"own": own, "after": [b.checksum() for b in bufs]})
+        identical = all(g["after"][r] == got[r]["own"] for g in got for r in range(world))
         dist.barrier()
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -323,6 +335,7 @@ def depth_exchange(args, ctx, rank, world, device, dist, allmax, reps=5):
         nbytes = 4 * args.width * args.height
         return {"ms_per_exchange": round(dt * 1e3, 3), "maps": world, "MB_per_map": round(nbytes / 1e6, 2),
                 "received_GBps_per_rank": round(nbytes * (world - 1) / dt / 1e9, 2), "maps_finite": bool(ok),
+                "maps_bit_identical": bool(identical), "map_checksums": [f"{g['own']:016x}" for g in got],
                 "transport": "RCCL grouped ncclBroadcast over xGMI (acmmp_comm_broadcast)"}
     except Exception as e:                                           # noqa: BLE001
         return {"error": f"{type(e).__name__}: {e}"}
@@ -444,6 +457,7 @@ def pipeline_mode(args, rank, world, local_rank, barrier, allmax):
         "passes": passes, "stages_s": stages,
         "exchange": "pipeline.RcclExchange (grouped ncclBroadcast, HBM to HBM)" if world > 1 else
                     "none: one rank holds every view (no scaling curve from this run)",
+        "maps_verified": getattr(exchange, "maps_verified", None),
         "scene_s": round(scene_s, 1),
         "quality": {"view0_frac_within_1pct_gt": round(float(acc[0]), 4) if acc else None},
     }
@@ -599,6 +613,27 @@ def main():
     elapsed = time.perf_counter() - t0
     t_max = allmax(elapsed)
 
+    # which GPU, and the clock it holds under a VALU-dense load right after the timed region (the chip's DVFS
+    # give-back differs from device to device, MI355X_MICROARCH.md; k_eval_nb's time follows that clock):
+    # reported so two records of the same build on different boxes can be put side by side per GHz
+    dev = local_rank % ndev if ndev else local_rank
+    ident = clk = None
+    try:
+        ident = capi.device_identity(dev)
+    except capi.AcmmpError as e:
+        ident = {"error": str(e)}
+    if not args.no_clock:
+        try:
+            clk = capi.clock_probe(dev, warm_ms=args.clock_warm_ms)
+        except capi.AcmmpError as e:
+            clk = {"error": str(e)}
+    if dist is not None:
+        got = [None] * world
+        dist.all_gather_object(got, {"rank": rank, "device": ident, "clock": clk})
+        ranks_hw = got
+    else:
+        ranks_hw = None
+
     # the other math mode on the same resident inputs (reported beside `value`, never `value`)
     other = None
     if not args.no_other_mode:
@@ -707,6 +742,8 @@ def main():
         "traffic": traffic,
         "kernel": "k_eval_nb (the 8 neighbour hypotheses of a CheckerboardPropagation half-sweep)",
         "launch_ms": round(launch_ms, 4),
+        # launch time in cycles of the probed clock: comparable across boxes whose clocks differ
+        "launch_mcycles_at_probe_clock": (round(launch_ms * clk["ghz"], 4) if clk and clk.get("ghz") else None),
         "launches": nb_n,
         "flop_per_launch": flop_launch,
         "evaluated_pixels_per_launch": round(pix_per_launch),
@@ -777,6 +814,14 @@ def main():
                 "note": "one rank: upload_views + run_patchmatch + download, host wall clock"},
             "quality": {"frac_within_1pct_gt": round(acc, 4), "nan_cost_frac": round(nan_frac, 4)},
             "roofline": roofline,
+            "device": ident,
+            "clock": None if clk is None else dict(clk, note=(
+                "acmmp_clock_probe right after the timed region: median over workgroups of shader cycles / 100 MHz "
+                "ticks around a VALU-dense loop on random operands, after warm_ms of such launches")),
+            "value_per_ghz": (round(value / clk["ghz"], 3) if clk and clk.get("ghz") and ranks_hw is None else
+                              (round(value / float(np.mean([r["clock"]["ghz"] for r in ranks_hw])), 3)
+                               if ranks_hw and all(r["clock"] and r["clock"].get("ghz") for r in ranks_hw) else None)),
+            "ranks_hw": ranks_hw,
             "cpu_baseline": cpu,
             "nondegenerate_variant": variant,
             "end_to_end": e2e,

@@ -260,6 +260,21 @@ acmmp_status acmmp_device_alloc(int device, size_t bytes, void **ptr);
 acmmp_status acmmp_device_free(int device, void *ptr);
 acmmp_status acmmp_memcpy(int device, void *dst, const void *src, size_t bytes, int kind);
 
+/* 64-bit checksum of `bytes` (a multiple of 4) of device memory on `device`: the sum mod 2^64 over its
+ * 32-bit words w_i of splitmix64's finaliser applied to (i << 32) | w_i (position and value both enter).
+ * The pipeline's depth exchange compares every rank's checksum of each broadcast map
+ * (acmmp/pipeline.py RcclExchange); acmmp.capi.checksum_host is the same function on host arrays. */
+acmmp_status acmmp_device_checksum(int device, const void *ptr, size_t bytes, uint64_t *out);
+
+/* Diagnostics for the performance record (bench.py `device`, `clock`); no reference counterpart.
+ * acmmp_device_identity: the device's PCI bus id ("dddd:bb:dd.f") and its 16-byte UUID.
+ * acmmp_clock_probe: the shader clock the device holds under a VALU-dense load on random operands
+ * (MI355X_MICROARCH.md "DVFS give-back"): ~5 ms launches back to back for warm_ms, then one launch whose
+ * workgroups read the shader-cycle and 100 MHz counters around their loop.  out = {median GHz over the
+ * workgroups, min, max, ms of that launch}.  Synchronous; uses the device's null stream. */
+acmmp_status acmmp_device_identity(int device, char *pci_bus_id, int len, uint8_t uuid[16]);
+acmmp_status acmmp_clock_probe(int device, float warm_ms, double out[4]);
+
 /* RCCL communicator, one rank per process / GPU.  Rank 0 creates the id and hands the 128 bytes
  * to the other ranks out of band (the Python driver uses the launcher's TCP store). */
 acmmp_status acmmp_comm_unique_id(uint8_t id[ACMMP_COMM_ID_BYTES]);

@@ -29,13 +29,19 @@ def summarize(root):
     for path in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
         rows = list(csv.DictReader(open(path)))
         acc = defaultdict(float)
-        keyname = {}
+        keyname, dur = {}, {}
         for r in rows:
             k = (r["Dispatch_Id"], r["Counter_Name"])
             acc[k] += float(r["Counter_Value"])
             keyname[r["Dispatch_Id"]] = r["Kernel_Name"]
+            if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+                dur[r["Dispatch_Id"]] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
         for (d, c), v in acc.items():
             per[short_name(keyname[d])][c].append(v)
+            # the dispatch's effective shader clock: GRBM_GUI_ACTIVE (summed over the 8 XCDs) / 8 / duration
+            # (MI355X_MICROARCH.md "DVFS give-back"; reads high below ~0.3 ms dispatches)
+            if c == "GRBM_GUI_ACTIVE" and dur.get(d, 0) > 0:
+                per[short_name(keyname[d])]["effective_clock_ghz"].append(v / 8.0 / dur[d])
     out = {}
     for kern, cs in per.items():
         out[kern] = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -68,7 +74,7 @@ if __name__ == "__main__":
                 for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
                           "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "TCC_HIT", "TCC_MISS",
                           "TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "TCP_TCC_READ_REQ_LATENCY_sum",
-                          "TCP_PENDING_STALL_CYCLES_sum"):
+                          "TCP_PENDING_STALL_CYCLES_sum", "GRBM_GUI_ACTIVE", "effective_clock_ghz"):
                     if c in v:
                         kernels[k][c] = v[c]
                 # SURVEY.md §8d's secondary gather roof: the L1 (TCP) hit rate -- the share of TCP accesses that
