@@ -25,30 +25,49 @@ class _HostPool:
     them crawl (30 ms for a 800x600 view's planes + costs, 0.9 ms into a hugepage mapping,
     profiles/r05_d2h_probe.json), and a new mapping per download pays its page faults every time: a mapping
     comes back here when the last array (or view) on it is collected and the next download of that size
-    reuses its resident pages.  At most `cap` bytes are kept."""
+    reuses its resident pages.  At most `cap` bytes are kept idle (ACMMP_HOST_POOL_BYTES, default 1 GiB):
+    beyond it the least recently returned mappings are dropped, so sizes a pipeline no longer requests (an
+    earlier pyramid scale) do not stay held; release() drops them all."""
 
-    def __init__(self, cap: int = 4 << 30):
-        self.cap, self.held, self.free = cap, 0, {}
+    def __init__(self, cap: int | None = None):
+        if cap is None:
+            cap = int(os.environ.get("ACMMP_HOST_POOL_BYTES", str(1 << 30)))
+        self.cap, self.held = cap, 0
+        self.free = {}                      # size -> [mapping]; insertion order of `order` = recency
+        self.order = []                     # (size, mapping) in the order they came back, oldest first
         self.lock = threading.Lock()
 
     def take(self, n: int):
         with self.lock:
             lst = self.free.get(n)
             if lst:
+                mm = lst.pop()
+                self.order = [(k, m) for (k, m) in self.order if m is not mm]
                 self.held -= n
-                return lst.pop()
+                return mm
         mm = mmap.mmap(-1, n, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
         if hasattr(mmap, "MADV_HUGEPAGE"):
             mm.madvise(mmap.MADV_HUGEPAGE)
         return mm
 
     def give(self, mm, n: int):
-        # (called while the array still holds its buffer export: an unkept mapping is unmapped when the last
+        # (called while the array still holds its buffer export: a dropped mapping is unmapped when the last
         # reference goes, not closed here)
+        if n > self.cap:
+            return
         with self.lock:
-            if self.held + n <= self.cap:
-                self.free.setdefault(n, []).append(mm)
-                self.held += n
+            while self.held + n > self.cap and self.order:
+                k, old = self.order.pop(0)              # least recently returned first
+                self.free[k].remove(old)
+                self.held -= k
+            self.free.setdefault(n, []).append(mm)
+            self.order.append((n, mm))
+            self.held += n
+
+    def release(self):
+        """Drop every idle mapping (e.g. when a pipeline evicts a pyramid scale)."""
+        with self.lock:
+            self.free, self.order, self.held = {}, [], 0
 
 
 _POOL = _HostPool()
@@ -636,8 +655,8 @@ class Context:
 
     def debug_ncc_ref(self, px, py, planes):
         """The refinement's NCC (k_eval_ref's instance; fast SPHERE with V > 4 at the interpolation's sizes:
-        interpolated coordinates, the tail's per-sample costs where they fall back) of planes (n, 5, 4) at
-        pixels (px, py) -> costs (n, 5, V)."""
+        interpolated coordinates; where they fall back, the per-sample costs of k_nb_fix<1, true>'s entry code,
+        the production fallback path) of planes (n, 5, 4) at pixels (px, py) -> costs (n, 5, V)."""
         return self._debug_k(self.L.acmmp_debug_ncc_ref, 5, px, py, planes, "debug_ncc_ref")
 
 

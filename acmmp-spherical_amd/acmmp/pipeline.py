@@ -544,6 +544,7 @@ class Pipeline:
             del self._scaled[key]
         for key in [k for k in self._scaled_dev if k[1] != self.problems[k[0]].cur_image_size]:
             self._scaled_dev.pop(key).free()
+        capi._POOL.release()                 # idle download mappings are sized for the previous scale
 
     def _commit_pending(self):
         for key, view, arr, ctx in self._pending:

@@ -989,7 +989,16 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     const bool fixq = c->model == kSphere && c->math == ACMMP_MATH_FAST && c->tex16 && kp.interp && Pc < fix_max_pc;
     if (!fixq && c->model == kSphere && c->math == ACMMP_MATH_FAST && c->tex16 && kp.interp && Pc >= fix_max_pc) kp.interp = 0;
     const size_t nb_blocks = static_cast<size_t>(nb_block_count(kp.rows, kp.Wh, kp.nb_tile));
-    const size_t fix_cap = fixq ? (nb_blocks + kNbFixRegions - 1) / kNbFixRegions * kNbPix * 8 * static_cast<size_t>(kp.nb_chunk) : 0;
+    // the refinement's interpolated instance (fast SPHERE, V > 4) queues its survivors' fallback views of
+    // [0, ref_split) into the same regions after k_eval_nb's queue is drained: a region's k_eval_ref blocks x
+    // kRefSlots survivors x ref_split views.  The room is the larger of the two producers' worst cases (the
+    // split can exceed the view chunk: ACMMP_REF_SPLIT_AT / ACMMP_NB_VIEW_CHUNK)
+    const int ref_split = ref_split_point(kp.V, Pc, kp.model == kSphere && c->math == ACMMP_MATH_FAST && c->tex16 &&
+                                                        kp.interp && kp.V > 4);
+    const size_t ref_blocks = (static_cast<size_t>(kp.rows) * kp.Wh + kRefPix - 1) / kRefPix;
+    const size_t fix_cap = !fixq ? 0 : std::max(
+        (nb_blocks + kNbFixRegions - 1) / kNbFixRegions * kNbPix * 8 * static_cast<size_t>(kp.nb_chunk),
+        (ref_blocks + kNbFixRegions - 1) / kNbFixRegions * kRefSlots * static_cast<size_t>(std::max(ref_split, 0)));
     // half-sweep scratch slab: carve the pieces of engine.h's KParams out of one allocation
     size_t off[18];
     {
@@ -1044,7 +1053,7 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.surv_dense = reinterpret_cast<uint32_t*>(c->d_scratch + off[15]);
     kp.cand_rough = reinterpret_cast<uint32_t*>(c->d_scratch + off[16]);
     kp.nbfix_cap = static_cast<unsigned>(fix_cap);
-    kp.ref_split = ref_split_point(kp.V, Pc, kp.model == kSphere && kp.fast && kp.tex16 && kp.interp && kp.V > 4);
+    kp.ref_split = ref_split;
     if (!c->d_work) HIP_TRY(c, dalloc(c->d_work, 257));
     kp.work = c->d_work;
     kp.status = reinterpret_cast<unsigned*>(c->d_work + 256);

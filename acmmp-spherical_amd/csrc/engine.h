@@ -28,6 +28,9 @@ constexpr int kSphere = 11;
 constexpr int kMaxViews = 32;       // cost_vector[32], uint32 view bitmask (ACMMP.cu:522,1153)
 constexpr int kNbPix = 32;          // k_eval_nb: pixels per 256-lane block (8 lanes each)
 constexpr int kNbFixRegions = 256;  // the queue's regions, one counter each (block % regions)
+constexpr int kRefLanes = 5;        // k_eval_ref: refinement candidates (ACMMP.cu:870)
+constexpr int kRefPix = 51;         // k_eval_ref: pixels per 256-lane block (255 lanes used)
+constexpr int kRefSlots = kRefPix * kRefLanes;  // survivor slots per k_eval_ref block
 constexpr unsigned kStatusFixOverflow = 1u;   // KParams::status: k_nb_fix found a region's queue overfull
 
 struct DevCam {

@@ -1845,9 +1845,7 @@ template <int MODEL, int VB, int TF>
 constexpr int ref_vb_eval() {
     return (MODEL == kPinhole && TF == 2 && ref_vb<MODEL, VB>() > 2) ? 2 : ref_vb<MODEL, VB>();
 }
-constexpr int kRefLanes = 5;                // refinement candidates (ACMMP.cu:870)
-constexpr int kRefPix = 51;                 // pixels per 256-lane block (255 lanes used)
-constexpr int kRefSlots = kRefPix * kRefLanes;  // survivor slots per k_eval_ref block
+// kRefLanes / kRefPix / kRefSlots: engine.h (capi.cpp sizes the survivor and fallback queues from them)
 
 // Adaptive checkerboard sampling of every pixel of the colour, one direction per grid row: the
 // direction is wave-uniform here, where inside k_eval_nb (lane = direction) a wave walks all eight
@@ -2972,6 +2970,37 @@ hipError_t launch_eval_nb_views(const KParams& kp, int colour, hipStream_t s);
 hipError_t launch_select(const KParams& kp, int colour, int iter, hipStream_t s);
 hipError_t launch_eval_ref(const KParams& kp, int colour, hipStream_t s);
 
+// The hooks' deferred fallbacks: k_nb_fix's entry code (fix_row, fix_fold) for query pixels and planes.  LANES:
+// hypotheses per query (8: acmmp_debug_ncc_nb, k_eval_nb's layout; 5: acmmp_debug_ncc_ref, the refinement's
+// candidates, whose production fallbacks run k_nb_fix<1, true>).  out[(q * LANES + h) * V + v].
+template <int TEX, int LANES>
+__global__ __launch_bounds__(256) void k_debug_nb_fix(const KParams kp, const int* __restrict__ qx,
+                                                      const int* __restrict__ qy, const float4* __restrict__ planes,
+                                                      float* __restrict__ out) {
+    __shared__ float4 smp[kFixPerBlock][36];
+    const int t = threadIdx.x, l = t & 63;
+    const int ew = l / kFixLanes, j = l - ew * kFixLanes, e = (t >> 6) * kFixPerWave + ew;
+    const unsigned region = blockIdx.x % kNbFixRegions, stripes = gridDim.x / kNbFixRegions;
+    const unsigned n = min(kp.nbfix_count[region], kp.nbfix_cap);
+    const uint32_t* qu = kp.nbfix + static_cast<long long>(region) * kp.nbfix_cap;
+    for (unsigned i0 = (blockIdx.x / kNbFixRegions) * kFixPerBlock; i0 < n; i0 += stripes * kFixPerBlock) {
+        const unsigned i = i0 + static_cast<unsigned>(e);
+        const bool act = ew < kFixPerWave && i < n;
+        long long k = 0;
+        int v = 0;
+        if (act) {
+            const uint32_t key = qu[i];
+            const int qq = static_cast<int>(key >> 8), h = static_cast<int>((key >> 5) & 7u);
+            v = static_cast<int>(key & 31u);
+            k = static_cast<long long>(qq) * LANES + h;
+            fix_row<TEX>(kp, qx[qq], qy[qq], planes[k], v, j, smp[e]);
+        }
+        __syncthreads();
+        if (act && j == 0) out[k * kp.V + v] = fix_fold(smp[e]);
+        __syncthreads();
+    }
+}
+
 #if ACMMP_IN_TU(2)
 // View-chunked k_eval_nb: one launch per chunk of 8 source views when the sources' texels outgrow the
 // 256 MB Infinity Cache, so all waves in flight sample the same few images (r02 A/B
@@ -3049,35 +3078,6 @@ __global__ __launch_bounds__(256) void k_debug_nb(const KParams kp, int n, const
         kp, px, py, pt, ph, all, [&](int v, float c) { o[v] = c; }, fixkey);
 }
 
-// The hook's deferred fallbacks (k_nb_fix for query pixels and planes)
-template <int TEX>
-__global__ __launch_bounds__(256) void k_debug_nb_fix(const KParams kp, const int* __restrict__ qx,
-                                                      const int* __restrict__ qy, const float4* __restrict__ planes,
-                                                      float* __restrict__ out) {
-    __shared__ float4 smp[kFixPerBlock][36];
-    const int t = threadIdx.x, l = t & 63;
-    const int ew = l / kFixLanes, j = l - ew * kFixLanes, e = (t >> 6) * kFixPerWave + ew;
-    const unsigned region = blockIdx.x % kNbFixRegions, stripes = gridDim.x / kNbFixRegions;
-    const unsigned n = min(kp.nbfix_count[region], kp.nbfix_cap);
-    const uint32_t* qu = kp.nbfix + static_cast<long long>(region) * kp.nbfix_cap;
-    for (unsigned i0 = (blockIdx.x / kNbFixRegions) * kFixPerBlock; i0 < n; i0 += stripes * kFixPerBlock) {
-        const unsigned i = i0 + static_cast<unsigned>(e);
-        const bool act = ew < kFixPerWave && i < n;
-        long long k = 0;
-        int v = 0;
-        if (act) {
-            const uint32_t key = qu[i];
-            const int qq = static_cast<int>(key >> 8), h = static_cast<int>((key >> 5) & 7u);
-            v = static_cast<int>(key & 31u);
-            k = static_cast<long long>(qq) * kNbLanes + h;
-            fix_row<TEX>(kp, qx[qq], qy[qq], planes[k], v, j, smp[e]);
-        }
-        __syncthreads();
-        if (act && j == 0) out[k * kp.V + v] = fix_fold(smp[e]);
-        __syncthreads();
-    }
-}
-
 hipError_t launch_debug_nb(const KParams& kp0, int n, const int* px, const int* py, const float4* planes, float* out,
                            hipStream_t s) {
     // the hook takes k_eval_nb's path, deferred fallbacks included
@@ -3098,7 +3098,7 @@ hipError_t launch_debug_nb(const KParams& kp0, int n, const int* px, const int* 
         if (kp.tex16) ACMMP_DISPATCH(kp.model, kp.V, (k_debug_nb<M, VBC, 1, 0><<<grd, 256, lds_nb, s>>>(kp, n, px, py, planes, out)));
         else ACMMP_DISPATCH(kp.model, kp.V, (k_debug_nb<M, VBC, 0, 0><<<grd, 256, lds_nb, s>>>(kp, n, px, py, planes, out)));
     }
-    if (fix) k_debug_nb_fix<1><<<kNbFixRegions, 256, 0, s>>>(kp, px, py, planes, out);
+    if (fix) k_debug_nb_fix<1, kNbLanes><<<kNbFixRegions, 256, 0, s>>>(kp, px, py, planes, out);
     return hipGetLastError();
 }
 
@@ -3181,8 +3181,9 @@ hipError_t launch_eval_ref(const KParams& kp0, int colour, hipStream_t s) {
 
 // Test hook (acmmp_debug_ncc_ref): the refinement's NCC on given queries of one pixel and 5 planes (the 5
 // candidates of PlaneHypothesisRefinement, ACMMP.cu:797-936) -- k_eval_ref's staging and NCC instance over
-// all views, and for the views whose interpolation fell back (fast SPHERE, V > 4) the per-sample arithmetic
-// k_eval_ref_tail recomputes them with.  out[(q * 5 + h) * V + v].
+// all views; the views whose interpolation fell back (fast SPHERE, V > 4) are queued as k_eval_ref queues a
+// survivor's (candidate << 5 | view keys on the fallback queue) and recomputed by k_debug_nb_fix<1, 5>, whose
+// per-entry code (fix_row, fix_fold) is k_nb_fix<1, true>'s.  out[(q * 5 + h) * V + v].
 template <int MODEL, int VB, int TF>
 __global__ __launch_bounds__(256) void k_debug_ref(const KParams kp, int n, const int* __restrict__ qx,
                                                    const int* __restrict__ qy, const float4* __restrict__ planes,
@@ -3208,15 +3209,25 @@ __global__ __launch_bounds__(256) void k_debug_ref(const KParams kp, int n, cons
     for_all_views_tf<MODEL, VBA, kStaged, kRefPipe, TF>(kp, px, py, pt, ph, all, [&](int v, float c) {
         o[v] = c;
         if (kRefInterp && c != c) rough |= 1u << v;
-    }, kRefInterp ? kFixNan : kFixNone);
-    if (kRefInterp) {
-        const uint32_t um = wave_or(rough, kp.V);
-        if (um) {
-            const Patch pu = make_patch<MODEL>(kp, px, py);
-            constexpr int VBT = (MODEL == kSphere && VB > 4) ? ACMMP_TAIL_SPH_VB : ref_vb<MODEL, VB>();
-            for_all_views_tf<MODEL, VBT, 0, kRefPipe, TF>(kp, px, py, pu, ph, um, [&](int v, float c) {
-                if ((rough >> v) & 1u) o[v] = c;
-            });
+    }, kRefInterp && kp.nbfix ? kFixNan : kFixNone);
+    if (kRefInterp && kp.nbfix) {
+        const unsigned long long any = __ballot(rough != 0u);
+        if (any) {
+            const int lane = lane_id_here();
+            const unsigned region = blockIdx.x % kNbFixRegions;
+            for (int v = 0; v < kp.V; ++v) {
+                const bool redo = (rough >> v) & 1u;
+                const unsigned long long b = __ballot(redo);
+                if (!b) continue;
+                const int leader = __ffsll(static_cast<long long>(b)) - 1;
+                unsigned base = 0u;
+                if (lane == leader) base = atomicAdd(kp.nbfix_count + region, static_cast<unsigned>(__popcll(b)));
+                base = __builtin_amdgcn_readlane(base, leader);
+                const unsigned slot = base + static_cast<unsigned>(__popcll(b & ((1ull << lane) - 1ull)));
+                if (redo && slot < kp.nbfix_cap)
+                    kp.nbfix[static_cast<long long>(region) * kp.nbfix_cap + slot] =
+                        (static_cast<uint32_t>(q) << 8) | (static_cast<uint32_t>(h) << 5) | static_cast<uint32_t>(v);
+            }
         }
     }
 }
@@ -3228,7 +3239,15 @@ hipError_t launch_debug_ref(const KParams& kp0, int n, const int* px, const int*
     const size_t lds_ref = (kp.model == kSphere && pick_vb(kp.V) <= 4) ? sep_lds_bytes(kp.S, kp.nside, kRefPix)
                                                                        : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
     const dim3 grd = static_cast<unsigned>(cdiv(n, kRefPix));
+    // the interpolated instance's fallbacks on the context's queue: room for every entry (a region's blocks x
+    // 255 candidates x V views), else the hook refuses
+    const bool fix = kp.interp && kp.nbfix && kp.model == kSphere && kp.fast && kp.tex16 && kp.V > 4 && n < (1 << 24);
+    if (!fix) kp.nbfix = nullptr;
+    if (fix && static_cast<long long>(cdiv(grd.x, kNbFixRegions)) * kRefSlots * kp.V > kp.nbfix_cap) return hipErrorInvalidValue;
+    hipError_t e0 = hipSuccess;
+    if (fix && (e0 = hipMemsetAsync(kp.nbfix_count, 0, sizeof(unsigned) * kNbFixRegions, s)) != hipSuccess) return e0;
     ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_debug_ref<M, VBC, TF><<<grd, 256, lds_ref, s>>>(kp, n, px, py, planes, out))));
+    if (fix) k_debug_nb_fix<1, kRefLanes><<<kNbFixRegions, 256, 0, s>>>(kp, px, py, planes, out);
     return hipGetLastError();
 }
 #endif  // ACMMP_IN_TU(4)

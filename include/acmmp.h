@@ -393,8 +393,9 @@ acmmp_status acmmp_debug_ncc_nb(acmmp_ctx *ctx, int n, const int *px, const int 
 /* costs[(k*5 + h)*(num_images-1) + v]: the same NCC of plane planes[k*5 + h] at pixel (px[k], py[k]) as
  * PlaneHypothesisRefinement (ACMMP.cu:797-936) evaluates its 5 candidates -- k_eval_ref's staging and NCC
  * instance, which in the fast math mode interpolates SPHERE sample coordinates above 4 source views (the
- * size gate of acmmp_debug_ncc_nb), and for the views whose interpolation falls back the per-sample costs
- * k_eval_ref_tail recomputes them with. */
+ * size gate of acmmp_debug_ncc_nb); the views whose interpolation falls back are queued as k_eval_ref queues
+ * them and recomputed with every sample projected by the per-entry code of k_nb_fix<1, true>, the
+ * production path of those fallbacks. */
 acmmp_status acmmp_debug_ncc_ref(acmmp_ctx *ctx, int n, const int *px, const int *py, const float *planes,
                                  float *costs);
 /* out[k*(num_images-1) + v] = ComputeGeomConsistencyCost (ACMMP.cu:646-671). */

@@ -97,3 +97,21 @@ def test_host_empty_download_arrays():
     b = capi.host_empty((800, 600, 4), np.float32)
     assert b.ctypes.data == ptr                         # ... and reused by the next array of that size
     assert capi.host_empty((600, 800), np.uint32).dtype == np.uint32
+
+
+def test_host_pool_cap_evicts_least_recent():
+    """_HostPool keeps at most `cap` idle bytes, dropping the least recently returned mappings first, and
+    release() drops them all (sizes of earlier pyramid scales must not stay held)."""
+    pool = capi._HostPool(cap=3 << 20)
+    a, b, c = pool.take(1 << 20), pool.take(2 << 20), pool.take(1 << 20)
+    pool.give(a, 1 << 20)
+    pool.give(b, 2 << 20)
+    assert pool.held == 3 << 20
+    pool.give(c, 1 << 20)                     # over the cap: a (oldest) goes
+    assert pool.held == 3 << 20 and pool.take(1 << 20) is c
+    assert pool.take(2 << 20) is b and pool.held == 0
+    pool.give(pool.take(8 << 20), 8 << 20)    # larger than the cap: never kept
+    assert pool.held == 0
+    pool.give(a, 1 << 20)
+    pool.release()
+    assert pool.held == 0 and pool.take(1 << 20) is not a

@@ -25,15 +25,18 @@ bit-identical, so it is held to the gates DESIGN.md §2.4 states, measured in pr
       is below 1e-4.  Where the fast kernels interpolate SPHERE sample coordinates (>= 2000x1000), the
       98.5% holds for the per-sample fast arithmetic (ACMMP_INTERP=0), and over four seeds the
       interpolated runs hold >= 98.5% same planes on average, at most 0.2 pt fewer than the per-sample
-      runs, with every seed's flips near ties (median cost gap < 3e-5; the float64 study puts the
+      runs, every seed at most 0.5 pt below its per-sample run, with every seed's flips near ties (median
+      cost gap < 3e-5; the float64 study puts the
       interpolation's NCC effect below 1e-4, tests/test_interp_design.py; the flips it adds are ties the
       binary32 noise already decides).  Measured: metric 98.58% vs 98.72%, C3 98.95% vs 99.05%
       (profiles/r05_t2_seeds.json).
   T3  A full RunPatchMatch: >= 99% of finite depths within 1% of the exact mode's, ground-truth accuracy
-      within +-0.5 points.  Geom, planar-prior and hierarchy passes from one shared state: T3, T2's init
-      gates, and after one half-sweep >= 85% same plane (the hierarchy gate and the prior-restricted
-      acceptance multiply near ties; a flip there selects by restricted cost or pre-cost, so its cost gap
-      is not a tie measure and is not gated).
+      within +-0.5 points.  Geom, planar-prior and hierarchy passes from one shared state (pinhole, SPHERE,
+      and SPHERE at the interpolation's size): T3, T2's init gates, and after one half-sweep, for each of
+      four seeds, the same plane on at least the measured four-seed mean - 0.5 pt of pixels
+      (profiles/r06_pass_gates.json); the geom pass's flips are near cost ties (median gap bounded as
+      measured); a planar / hierarchy flip selects by restricted cost or pre-cost, so its cost gap is not
+      a tie measure and is not gated.
 """
 import json
 import os
@@ -203,6 +206,9 @@ def test_fast_mode_tolerance_at_baseline_configs(ctx, config, monkeypatch):
         ps_mean = float(np.mean([r[0] for r in per_sample]))
         ip_mean = float(np.mean([r[0] for r in interpolated]))
         assert ip_mean >= 0.985 and ip_mean >= ps_mean - 0.002, (ip_mean, ps_mean)
+        # and no seed far below its per-sample run (a mean can hide one seed's regression)
+        for seed, a, b in zip(seeds, per_sample, interpolated):
+            assert b[0] >= a[0] - 0.005, (seed, b[0], a[0])
         for seed, a, b in zip(seeds, per_sample, interpolated):
             report[f"per_sample_seed{seed}"] = a
             report[f"interpolated_seed{seed}"] = b
@@ -219,13 +225,14 @@ def test_fast_mode_tolerance_at_baseline_configs(ctx, config, monkeypatch):
 
 
 PASS_RIGS = {"pinhole": lambda: scene.pinhole_scene(800, 600, n_src=10, seed=61, n_waves=24),
-             "sphere": lambda: scene.sphere_scene(1000, 500, n_src=6, seed=62, n_waves=24)}
+             "sphere": lambda: scene.sphere_scene(1000, 500, n_src=6, seed=62, n_waves=24),
+             # the interpolated coordinates (k_eval_nb, and k_eval_ref above 4 views) in every pass kind
+             "sphere-interp": lambda: scene.sphere_scene(2000, 1000, n_src=6, seed=63, n_waves=24)}
 
 
-@pytest.fixture(scope="module", params=list(PASS_RIGS))
-def pass_rig(request, ctx):
+def make_pass_rig(ctx, name):
     """A random first pass in the exact mode: the state the geom / planar / hierarchy passes start from."""
-    sc = PASS_RIGS[request.param]()
+    sc = PASS_RIGS[name]()
     H, W = sc.images[0].shape
     V = len(sc.images) - 1
     p0 = params_for(sc)
@@ -240,14 +247,43 @@ def pass_rig(request, ctx):
     ctx.set_state(first_p, first_c)
     ctx.set_planar_prior_from_maps(first_p[..., 3], first_c, float(p0["depth_min"]), float(p0["depth_max"]))
     prior, masks = ctx.download_planar_prior()
-    return request.param, sc, first_p, first_c, depths, prior, masks
+    return name, sc, first_p, first_c, depths, prior, masks
 
 
-@pytest.mark.parametrize("kind", ["geom", "planar", "hierarchy"])
-def test_fast_mode_tolerance_in_geom_planar_hierarchy_passes(ctx, pass_rig, kind):
-    model, sc, first_p, first_c, depths, prior, masks = pass_rig
+@pytest.fixture(scope="module", params=list(PASS_RIGS))
+def pass_rig(request, ctx):
+    return make_pass_rig(ctx, request.param)
+
+
+# After one half-sweep of a geom / planar / hierarchy pass from the shared first-pass state, the share of pixels
+# whose fast-mode plane equals the exact mode's, over seeds 72-75 (scripts/pass_gates.py,
+# profiles/r06_pass_gates.json): the floor is the measured four-seed mean - 0.5 pt per (rig, pass kind), and each
+# seed's share must hold it.  In the geom pass a flip is still decided by cost (the geometric term is added to it,
+# ACMMP.cu:1210-1228), so its median |cost gap| is gated too; the planar (prior-restricted acceptance by restricted
+# cost, :1247-1299) and hierarchy (pre-cost gate, :1315-1324) flips are not cost ties and their gap is not a tie
+# measure.
+PASS_SEEDS = (72, 73, 74, 75)
+PASS_FLOORS = {}              # (rig, kind) -> same-plane floor; filled from profiles/r06_pass_gates.json below
+GEOM_GAP_MAX = {}             # rig -> median flip cost gap bound of the geom pass
+
+
+def _load_pass_gates():
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r06_pass_gates.json")
+    if not os.path.exists(path):
+        return
+    d = json.load(open(path))
+    for rig, kinds in d["measured"].items():
+        for kind, m in kinds.items():
+            PASS_FLOORS[(rig, kind)] = round(m["same_plane_mean"] - 0.005, 4)
+            if kind == "geom":
+                GEOM_GAP_MAX[rig] = m["gap_bound"]
+
+
+_load_pass_gates()
+
+
+def pass_setup(kind, sc, first_p, first_c, depths, prior, masks):
     H, W = sc.images[0].shape
-
     if kind == "geom":
         def setup(c):
             c.set_params(params_for(sc, geom_consistency=1, max_iterations=2))
@@ -274,8 +310,26 @@ def test_fast_mode_tolerance_in_geom_planar_hierarchy_passes(ctx, pass_rig, kind
             c.upload_views(sc.images, sc.cameras)
             c.set_state(cur, zc)
             c.set_scaled_state(coarse)
-    check_t2(ctx, setup, 72, model == "sphere", init=True, hs_min=0.85, gap_max=None)
+    return setup
+
+
+@pytest.mark.parametrize("kind", ["geom", "planar", "hierarchy"])
+def test_fast_mode_tolerance_in_geom_planar_hierarchy_passes(ctx, pass_rig, kind):
+    rig, sc, first_p, first_c, depths, prior, masks = pass_rig
+    setup = pass_setup(kind, sc, first_p, first_c, depths, prior, masks)
+    sphere = rig.startswith("sphere")
+    floor = PASS_FLOORS.get((rig, kind), 0.85)
+    gap_max = GEOM_GAP_MAX.get(rig) if kind == "geom" else None
+    got = []
+    for k, seed in enumerate(PASS_SEEDS):
+        got.append(check_t2(ctx, setup, seed, sphere, init=k == 0, hs_min=floor, gap_max=gap_max))
     check_t3(ctx, setup, 73, sc.gt_depth)
+    out_dir = os.environ.get("ACMMP_TEST_REPORT_DIR")
+    if out_dir:
+        os.makedirs(out_dir, exist_ok=True)
+        with open(os.path.join(out_dir, f"pass_t2_{rig}_{kind}.json"), "w") as fh:
+            json.dump({"floor": floor, "gap_max": gap_max, "seeds": list(PASS_SEEDS),
+                       "same_plane": [g[0] for g in got], "flip_median_cost_gap": [g[1] for g in got]}, fh, indent=1)
 
 
 def test_fast_mode_is_deterministic(ctx):

@@ -262,7 +262,8 @@ def refinement_planes(sc, px, py, seed):
 def test_interpolated_refinement_per_query(ctx, name, monkeypatch):
     """acmmp_debug_ncc_ref runs k_eval_ref's staging and NCC instance -- which in the fast mode interpolates SPHERE
     sample coordinates above 4 source views -- and, for the views whose interpolation nodes spread too far, the
-    per-sample costs k_eval_ref_tail recomputes them with (kernels.hip k_eval_ref / k_eval_ref_tail).  Held per
+    per-sample costs of the production fallback's entry code (queued as k_eval_ref queues them, recomputed by
+    k_nb_fix<1, true>'s fix_row / fix_fold).  Held per
     query on the pole / seam / random sets against: the per-sample fast hook (bit for bit where every entry falls
     back, ACMMP_SPREAD_MAX=-1), the exact mode (k_eval_ref's exact instance = the per-sample exact hook bit for
     bit) and float64 (np_reference.bilateral_ncc; T1's gates of test_gpu_fastmath.check_t1)."""
@@ -293,7 +294,7 @@ def test_interpolated_refinement_per_query(ctx, name, monkeypatch):
         re_ = ctx.debug_ncc_ref(px, py, planes)
         ps_e = ctx.debug_ncc(flat_x, flat_y, planes.reshape(-1, 4)).reshape(rf.shape)
         assert not np.isnan(rf).any() and not np.isnan(every).any()
-        # every entry deferred: the per-sample fast NCC bit for bit (the tail's arithmetic)
+        # every entry deferred: the per-sample fast NCC bit for bit (k_nb_fix's arithmetic)
         bad = np.nonzero(every.view(np.uint32) != ps_f.view(np.uint32))
         assert bad[0].size == 0, (kind, bad[0].size)
         # k_eval_ref's exact instance is the per-sample exact NCC bit for bit (the oracle's arithmetic)

@@ -158,6 +158,25 @@ def test_gpu_pipeline_overlapped_planar_passes_equal_sequential(math, slots):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("math", ["exact", "fast"])
+def test_gpu_pipeline_snapshot_geom_overlap_equals_sequential(math):
+    """Snapshot order (what sharded runs use) with geom_iterations 2: the geom passes, multi-geometry ones
+    included, run overlapped on several contexts (the default) and store exactly what the sequential loop
+    stores (the overlap-vs-sequential test covered only the reference order)."""
+    ds = small_dataset(64, 32, 5)
+    a = pipeline.Pipeline(ds, order="snapshot", size_bound=40, math=math, geom_iterations=2).run()
+    b = pipeline.Pipeline(ds, order="snapshot", size_bound=40, math=math, geom_iterations=2, overlap=False).run()
+    assert a._engine2 is not None and b._engine2 is None
+    assert any(p.name.startswith("geom") for p in a.passes)
+    ma, mb = final_maps(a), final_maps(b)
+    assert ma.keys() == mb.keys() and len(ma) >= 20
+    for k in mb:
+        assert_bitwise_equal(ma[k], mb[k], str(k))
+    a.close()
+    b.close()
+
+
+@pytest.mark.gpu
 def test_rccl_single_rank_comm_and_device_store():
     """The RCCL communicator and device buffers of the exchange path on one rank (multi-rank runs
     need one GPU per rank: RCCL refuses two ranks on one device)."""
@@ -185,6 +204,15 @@ def test_rccl_single_rank_comm_and_device_store():
         comm.broadcast([dbuf], [0])
         assert_bitwise_equal(dbuf.download(), planes[..., 3], "exported depth after the broadcast")
         dbuf.free()
+        # RcclExchange.share with its payload check (device checksums before / after, compared over the comm)
+        store = pipeline.ViewStore(0)
+        store.put("depths", 0, planes[..., 3], ctx=ctx)
+        ex = pipeline.RcclExchange(comm, 0, verify=True)
+        ex.share("depths", [0], {0: 0}, store)
+        assert ex.maps_verified == 1
+        assert store.dev[("depths", 0)].checksum() == capi.checksum_host(np.ascontiguousarray(planes[..., 3]))
+        for b in store.dev.values():
+            b.free()
     comm.close()
     buf.free()
 
