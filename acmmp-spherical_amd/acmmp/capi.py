@@ -100,7 +100,7 @@ EXPORTS = [
     "acmmp_set_params", "acmmp_upload_views", "acmmp_upload_depths", "acmmp_set_state",
     "acmmp_set_scaled_state", "acmmp_set_planar_prior", "acmmp_run_patchmatch", "acmmp_run_patchmatch_ex",
     "acmmp_download", "acmmp_download_aux", "acmmp_device_outputs", "acmmp_synchronize", "acmmp_last_timing",
-    "acmmp_last_kernel_timing", "acmmp_last_work", "acmmp_texel_bytes", "acmmp_set_math", "acmmp_get_math", "acmmp_jbu",
+    "acmmp_last_kernel_timing", "acmmp_last_work", "acmmp_last_planar_timing", "acmmp_texel_bytes", "acmmp_set_math", "acmmp_get_math", "acmmp_jbu",
     "acmmp_debug_ncc", "acmmp_debug_geom", "acmmp_debug_ncc_nb", "acmmp_debug_ncc_ref",
     "acmmp_support_points", "acmmp_delaunay", "acmmp_prior_plane_params", "acmmp_depth_from_plane_param",
     "acmmp_planar_prior_host", "acmmp_set_planar_prior_from_maps", "acmmp_set_planar_prior_from_state",
@@ -156,6 +156,7 @@ def load_library(path: str = LIB_PATH):
     L.acmmp_last_timing.argtypes = [vp, vp]
     L.acmmp_last_kernel_timing.argtypes = [vp, vp, vp]
     L.acmmp_last_work.argtypes = [vp, vp, vp]
+    L.acmmp_last_planar_timing.argtypes = [vp, vp]
     L.acmmp_texel_bytes.argtypes = [vp]
     L.acmmp_set_math.argtypes = [vp, i32]
     L.acmmp_get_math.argtypes = [vp]
@@ -613,6 +614,13 @@ class Context:
         e, t = C.c_ulonglong(0), C.c_ulonglong(0)
         self._check(self.L.acmmp_last_work(self.h, C.byref(e), C.byref(t)), "last_work")
         return e.value, t.value
+
+    def last_planar_timing(self):
+        """Host wall ms of the last set_planar_prior_from_state / _from_maps: support points, triangles (Delaunay +
+        plane fits on the host), device half (upload, raster, mask)."""
+        ms = np.zeros(3, np.float32)
+        self._check(self.L.acmmp_last_planar_timing(self.h, _p(ms)), "last_planar_timing")
+        return {"support_ms": float(ms[0]), "triangles_ms": float(ms[1]), "device_ms": float(ms[2])}
 
     def texel_bytes(self) -> int:
         """Bytes per source texel the NCC fetches read (2: binary16 copy, 4: fp32, 0: no views)."""

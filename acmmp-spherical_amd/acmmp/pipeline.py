@@ -671,11 +671,13 @@ class Pipeline:
                 with self._timed("planar_prior"):
                     e.set_params(p)
                     e.set_planar_prior_from_state(float(p["depth_min"]), float(p["depth_max"]))
+                self._planar_parts(e)
             elif hasattr(e, "set_planar_prior_from_maps"):
                 # support points + Delaunay + planes on the host, raster + mask on the device
                 with self._timed("planar_prior"):
                     e.set_params(p)
                     e.set_planar_prior_from_maps(planes[..., 3], costs, float(p["depth_min"]), float(p["depth_max"]))
+                self._planar_parts(e)
             else:
                 with self._timed("planar_prior"):
                     prior, masks, _ = capi.planar_prior_host(c0, planes[..., 3], costs, float(p["depth_min"]),
@@ -706,6 +708,16 @@ class Pipeline:
                 io.write_dmb(os.path.join(d, "normals.dmb"), planes[..., :3])
                 io.write_dmb(os.path.join(d, "costs.dmb"), costs)
         return planes, costs
+
+    def _planar_parts(self, e):
+        """The planar_prior stage's split (support points / host triangles / device half), summed like it."""
+        if not hasattr(e, "last_planar_timing"):
+            return
+        parts = e.last_planar_timing()
+        with self._stage_lock:
+            for k, ms in parts.items():
+                key = "planar_prior." + k[:-3]
+                self.stage_s[key] = self.stage_s.get(key, 0.0) + ms / 1e3
 
     @staticmethod
     def _state_planar(e):

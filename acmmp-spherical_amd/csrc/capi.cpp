@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -116,7 +117,8 @@ struct acmmp_ctx {
     size_t scratch_bytes = 0;
 
     float timing[3] = {0.f, 0.f, 0.f};
-    std::vector<hipEvent_t> kev;               // 5 per half-sweep (per-kernel timing)
+    float planar_ms[3] = {0.f, 0.f, 0.f};      // acmmp_last_planar_timing
+    std::vector<hipEvent_t> kev;              // 5 per half-sweep (per-kernel timing)
     float ktiming[4] = {0.f, 0.f, 0.f, 0.f};
     unsigned long long* d_work = nullptr;       // [256] k_eval_nb work counters + [256] the run's status word
     unsigned long long work_busy = 0, work_total = 0;
@@ -775,8 +777,14 @@ acmmp_status acmmp_set_planar_prior(acmmp_ctx* c, const float* prior, const uint
 
 // The device half of the planar block for host-computed triangles: one upload of the tables, the raster
 // and the prior-depth mask / expansion kernels, into the context's planar-prior state.
+using planar_clock = std::chrono::steady_clock;
+static float ms_since(planar_clock::time_point t0) {
+    return std::chrono::duration<float, std::milli>(planar_clock::now() - t0).count();
+}
+
 static acmmp_status upload_planar(acmmp_ctx* c, const PlanarTriangles& pt, float depth_min, float depth_max,
                                   int* n_triangles) {
+    const auto t0 = planar_clock::now();
     const acmmp_camera& cam = c->cams[0];
     const int W = c->W, H = c->H;
     const size_t P = P_of(c);
@@ -817,6 +825,7 @@ static acmmp_status upload_planar(acmmp_ctx* c, const PlanarTriangles& pt, float
     HIP_TRY(c, launch_planar_raster(pd, c->d_mask, c->stream));
     HIP_TRY(c, launch_planar_mask(pd, c->d_mask, c->d_prior, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));       // `host` is pageable and goes out of scope
+    c->planar_ms[2] = ms_since(t0);
     c->has_prior = true;
     if (n_triangles) *n_triangles = m;
     return ACMMP_OK;
@@ -827,9 +836,12 @@ acmmp_status acmmp_set_planar_prior_from_maps(acmmp_ctx* c, const float* depths,
     if (!c || !depths || !costs) return fail(c, ACMMP_ERR_INVALID_ARGUMENT, "null argument");
     if (c->N == 0) return fail(c, ACMMP_ERR_STATE, "upload_views first");
     HIP_TRY(c, hipSetDevice(c->device));
+    const auto t0 = planar_clock::now();
     PlanarTriangles pt;
     const acmmp_status st = planar_triangles(c->cams[0], depths, costs, c->W, c->H, &pt);
     if (st != ACMMP_OK) return fail(c, st, "planar_triangles");
+    c->planar_ms[0] = 0.f;                                  // the support-point scan is inside planar_triangles
+    c->planar_ms[1] = ms_since(t0);
     return upload_planar(c, pt, depth_min, depth_max, n_triangles);
 }
 
@@ -841,6 +853,7 @@ acmmp_status acmmp_set_planar_prior_from_state(acmmp_ctx* c, float depth_min, fl
     HIP_TRY(c, hipSetDevice(c->device));
     const int W = c->W, H = c->H;
     const size_t nb = static_cast<size_t>((W + 4) / 5) * ((H + 4) / 5);
+    const auto t0 = planar_clock::now();
     HIP_TRY(c, dreserve(c->d_support, c->support_cap, nb));
     HIP_TRY(c, launch_support_points(c->d_costs_rm, c->d_planes_rm, W, H, c->d_support, c->stream));
     std::vector<int4> blocks(nb);
@@ -856,9 +869,12 @@ acmmp_status acmmp_set_planar_prior_from_state(acmmp_ctx* c, float depth_min, fl
         std::memcpy(&d, &b.w, sizeof d);
         depth_at.push_back(d);
     }
+    c->planar_ms[0] = ms_since(t0);
+    const auto t1 = planar_clock::now();
     PlanarTriangles pt;
     const acmmp_status st = planar_triangles_pts(c->cams[0], xy, depth_at, W, H, &pt);
     if (st != ACMMP_OK) return fail(c, st, "planar_triangles");
+    c->planar_ms[1] = ms_since(t1);
     return upload_planar(c, pt, depth_min, depth_max, n_triangles);
 }
 
@@ -1356,6 +1372,12 @@ acmmp_status acmmp_synchronize(acmmp_ctx* c) {
 acmmp_status acmmp_last_timing(const acmmp_ctx* c, float ms[3]) {
     if (!c || !ms) return ACMMP_ERR_INVALID_ARGUMENT;
     for (int i = 0; i < 3; ++i) ms[i] = c->timing[i];
+    return ACMMP_OK;
+}
+
+acmmp_status acmmp_last_planar_timing(const acmmp_ctx* c, float ms[3]) {
+    if (!c || !ms) return ACMMP_ERR_INVALID_ARGUMENT;
+    for (int i = 0; i < 3; ++i) ms[i] = c->planar_ms[i];
     return ACMMP_OK;
 }
 

@@ -296,6 +296,27 @@ __device__ __forceinline__ f32x2 atan_core_fast2(f32x2 t) {
     return pk_fma(t * z, p, t);
 }
 
+// SPHERE: the source pixel of the direction (t.x, t.y, tz) in the source camera's frame.  Longitude =
+// atan2(tx, tz) (ProjectonCamera_cu :631) and -latitude = asin(ty / |t|) (:626-630) = atan2(ty, hypot(tx, tz)):
+// both through ONE packed atan over y = (tx, ty), x = (tz, h) -- the minimax atan of atan_core_fast
+// (1.1e-7 rad) for the latitude too, in place of the asin polynomial with its range reduction and square
+// root.  Invariant under a positive scale of the direction.
+template <typename Cam>
+__device__ __forceinline__ void sphere_pixel_fast(Cam& c, f32x2 t, float tz, float& ox, float& oy) {
+    const float h = __builtin_amdgcn_sqrtf(fmaf(tz, tz, t.x * t.x));
+    const f32x2 mn = (f32x2){min_abs(tz, t.x), min_abs(h, t.y)};
+    const f32x2 rc = (f32x2){__builtin_amdgcn_rcpf(max_abs(tz, t.x)), __builtin_amdgcn_rcpf(max_abs(h, t.y))};
+    f32x2 r = atan_core_fast2(mn * rc);
+    const f32x2 rq = splat2(kPio2Hi) - r;                          // |y| > |x|: pi/2 - atan(|x| / |y|)
+    r.x = fabsf(t.x) > fabsf(tz) ? rq.x : r.x;
+    r.y = fabsf(t.y) > h ? rq.y : r.y;
+    r.x = __builtin_bit_cast(int, tz) < 0 ? kPiHi - r.x : r.x;   // x < 0 (h >= 0 never is)
+    const f32x2 ang = (f32x2){copysignf(r.x, t.x), copysignf(r.y, t.y)};
+    const f32x2 o = pk_fma(ang, (f32x2){c.fkx, c.fky}, (f32x2){c.cx, c.cy});
+    ox = o.x;
+    oy = o.y;
+}
+
 // P: the sample's point in the REFERENCE camera's frame (depth * ray); FR / Ft map it into the source
 // camera (DevCam::FRxy / FRz / Ft, set per problem), so no world point is formed per sample.  Rows 0
 // and 1 of FR are interleaved in DevCam so (x, y) of the mapped point is one packed fma chain (the same
@@ -311,22 +332,7 @@ __device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float&
     t = pk_fma((f32x2){c.FRxy[4], c.FRxy[5]}, splat2(P.z), t);
     const float tz = fmaf(c.FRz[2], P.z, fmaf(c.FRz[1], P.y, fmaf(c.FRz[0], P.x, fz)));
     if (MODEL == kSphere) {
-        // longitude = atan2(tx, tz) (ProjectonCamera_cu :631) and -latitude = asin(ty / |t|) (:626-630)
-        // = atan2(ty, hypot(tx, tz)): both through ONE packed atan over y = (tx, ty), x = (tz, h) -- the
-        // minimax atan of atan_core_fast (1.1e-7 rad) for the latitude too, in place of the asin
-        // polynomial with its range reduction and square root
-        const float h = __builtin_amdgcn_sqrtf(fmaf(tz, tz, t.x * t.x));
-        const f32x2 mn = (f32x2){min_abs(tz, t.x), min_abs(h, t.y)};
-        const f32x2 rc = (f32x2){__builtin_amdgcn_rcpf(max_abs(tz, t.x)), __builtin_amdgcn_rcpf(max_abs(h, t.y))};
-        f32x2 r = atan_core_fast2(mn * rc);
-        const f32x2 rq = splat2(kPio2Hi) - r;                          // |y| > |x|: pi/2 - atan(|x| / |y|)
-        r.x = fabsf(t.x) > fabsf(tz) ? rq.x : r.x;
-        r.y = fabsf(t.y) > h ? rq.y : r.y;
-        r.x = __builtin_bit_cast(int, tz) < 0 ? kPiHi - r.x : r.x;   // x < 0 (h >= 0 never is)
-        const f32x2 ang = (f32x2){copysignf(r.x, t.x), copysignf(r.y, t.y)};
-        const f32x2 o = pk_fma(ang, (f32x2){c.fkx, c.fky}, (f32x2){c.cx, c.cy});
-        ox = o.x;
-        oy = o.y;
+        sphere_pixel_fast(c, t, tz, ox, oy);
         // |t| < 1e-6 (:618-622), a sample on a source camera's centre, is not tested: such a sample
         // projects to NaN and its view's cost is 2.0 (the NCC clamp) -- the reference's tex2D of
         // (cx, cy) there is as meaningless, and no real geometry reaches it
@@ -679,6 +685,11 @@ __device__ __forceinline__ void sphere_fold_sample(float w, float r, float sp, f
 //    through a pointer instead took k_eval_ref from 120 to 256 VGPRs.)
 // With kFixNone every sample is projected.
 constexpr uint32_t kFixNone = ~0u, kFixNan = ~0u - 1u;
+// the interpolation nodes through the plane's homography (ncc_chunk; 0 builds round 5's ray-plane depth + rigid
+// map per node for A/Bs)
+#ifndef ACMMP_NODE_HOMOG
+#define ACMMP_NODE_HOMOG 1
+#endif
 
 // The lane's index in its wave, read where it is used: an asm volatile statement is neither hoisted nor merged
 // with another read, so a value derived from it is not kept live from the prologue (k_eval_nb spilled its lane
@@ -813,12 +824,56 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             constexpr int kNode[4] = {0, 2, 3, 5};
             const float spread_max = kp.spread_max;     // source pixels spanned by the corner nodes (see below)
             uint32_t rough = 0u;                        // views whose nodes spread too far (below)
+#if ACMMP_NODE_HOMOG
+            // A node's source direction through the plane's homography (round 6): the node's point in the
+            // reference frame is d r with d = -w / (n . r), so its source-frame point is
+            //     t = d FR r + Ft = d (FR - Ft n^T / w) r = d M r,
+            // and longitude / latitude are invariant under the positive scale d: the node projects as M r --
+            // one 3x3 product per node and view (M formed once per view) instead of the ray-plane depth, the
+            // point and the rigid map (k_eval_nb's node part 22 -> 9 VALU slots per node-view).  That holds
+            // where every node's depth is positive and not at the fast depth's |n . r| < 1e-6 clamp (1e6):
+            // a hypothesis with a node outside it (a plane through the reference centre, or one so near
+            // grazing that its depth changes sign inside the patch -- whose nodes spread past spread_max in
+            // the per-sample arithmetic anyway) sends all its views to the per-sample fallback.  Checked once
+            // per hypothesis over the 16 node rays: depth > 0 <=> sign(w) (n . r) < 0.
+            {
+                const float sg = copysignf(1.0f, ph.w);
+                const float nx = ph.x * sg, ny = ph.y * sg, nz = ph.z * sg;
+                float emax = -3.0f;
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const float4 q = pt.rw[(kNode[a] * 6 + kNode[b]) * pt.stride];
+                        emax = fmaxf(emax, dot3(nx, ny, nz, q.x, pt.rr[kNode[b] * pt.stride], q.y));
+                    }
+                }
+                if (!(emax <= -1e-6f) || ph.w == 0.0f) rough = 0xffffffffu;
+            }
+            const float kw = -__builtin_amdgcn_rcpf(ph.w);   // -1 / w
+#endif
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
                 if (!has(v)) continue;
                 ConstCam& c = PCV(v);
                 const __amdgpu_buffer_rsrc_t rs =
                     __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000);
+#if ACMMP_NODE_HOMOG
+                // M = FR - Ft n^T / w, rows 0 and 1 interleaved per column as FRxy is
+                f32x2 Mxy[3];
+                float Mz[3];
+                {
+                    // scalar fmas: packed ones with splat operands had the splats hoisted out of the view loop as
+                    // register pairs and spilled
+                    const float fkx = c.Ft[0] * kw, fky = c.Ft[1] * kw, fkz = c.Ft[2] * kw;
+                    const float n3[3] = {ph.x, ph.y, ph.z};
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        Mxy[k] = (f32x2){fmaf(fkx, n3[k], c.FRxy[2 * k]), fmaf(fky, n3[k], c.FRxy[2 * k + 1])};
+                        Mz[k] = fmaf(fkz, n3[k], c.FRz[k]);
+                    }
+                }
+#endif
                 float x00 = 0.f;                            // the first node's x (set below)
                 // one patch column's six samples from its four row nodes (x, y): the bilinear tap and the
                 // sums of ACMMP.cu:488-498
@@ -901,9 +956,15 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                     for (int b = 0; b < 4; ++b) {
                         const float4 q = pt.rw[(kNode[a] * 6 + kNode[b]) * pt.stride];
                         const float4 rw = make_float4(q.x, pt.rr[kNode[b] * pt.stride], q.y, q.z);
-                        const float dep = depth_from_plane_fast(ph, rw);
                         float x, y;
+#if ACMMP_NODE_HOMOG
+                        const f32x2 hxy = pk_fma(Mxy[2], splat2(rw.z), pk_fma(Mxy[1], splat2(rw.y), Mxy[0] * splat2(rw.x)));
+                        const float hz = fmaf(Mz[2], rw.z, fmaf(Mz[1], rw.y, Mz[0] * rw.x));
+                        sphere_pixel_fast(c, hxy, hz, x, y);
+#else
+                        const float dep = depth_from_plane_fast(ph, rw);
                         project_fast<MODEL>(c, make_float3(rw.x * dep, rw.y * dep, rw.z * dep), x, y);
+#endif
                         if (a == 0 && b == 0) {
                             x00 = x;
                             nd[b].x = 0.0f;

@@ -213,6 +213,12 @@ acmmp_status acmmp_last_kernel_timing(const acmmp_ctx *ctx, float ms[4], int lau
  * (ACMMP.cu:501-503) and are short-circuited; the roofline counts only evaluated pixels. */
 acmmp_status acmmp_last_work(const acmmp_ctx *ctx, unsigned long long *evaluated, unsigned long long *total);
 
+/* Host wall-clock breakdown of the last acmmp_set_planar_prior_from_state / _from_maps call, in ms:
+ * [support points (device kernel + copy back, or host scan), triangles (Delaunay, plane fits and step
+ * tables on the host), device half (table upload, raster and mask kernels, until they complete)].
+ * No reference counterpart (profiling of main.cpp:113-187's block). */
+acmmp_status acmmp_last_planar_timing(const acmmp_ctx *ctx, float ms[3]);
+
 /* Bytes per source texel the NCC fetches read: 2 when every texel of the uploaded views is exactly
  * a binary16 number (8-bit images are) and the engine keeps a binary16 copy of them, 4 for the fp32
  * images, 0 before acmmp_upload_views.  Results are identical either way; the

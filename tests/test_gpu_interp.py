@@ -31,7 +31,9 @@ pytestmark = pytest.mark.gpu
 
 CONFIGS = {
     "metric-2000x1500-v4": (lambda: scene.sphere_scene(2000, 1500, n_src=4, seed=1234, n_waves=24), 8),
-    "c3-3200x1600-v15": (lambda: scene.sphere_scene(3200, 1600, n_src=15, seed=1234, n_waves=12), 2),
+    # (C3: every plane of each pixel against float64 too -- with 2 of 8 the seam set's T1 fractions moved by up to 0.015
+    # between builds of the same per-query accuracy, sampling noise, profiles/r06_nodeh_queries.txt)
+    "c3-3200x1600-v15": (lambda: scene.sphere_scene(3200, 1600, n_src=15, seed=1234, n_waves=12), 8),
 }
 KINDS = {"random": 40, "pole": 32, "seam": 32}
 
