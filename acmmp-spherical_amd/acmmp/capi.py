@@ -616,11 +616,12 @@ class Context:
         return e.value, t.value
 
     def last_planar_timing(self):
-        """Host wall ms of the last set_planar_prior_from_state / _from_maps: support points, triangles (Delaunay +
-        plane fits on the host), device half (upload, raster, mask)."""
-        ms = np.zeros(3, np.float32)
+        """Host wall ms of the last set_planar_prior_from_state / _from_maps: support points, Delaunay, the rest of
+        the host half (triangles, plane fits, tables), device half (staging + enqueueing upload, raster, mask)."""
+        ms = np.zeros(4, np.float32)
         self._check(self.L.acmmp_last_planar_timing(self.h, _p(ms)), "last_planar_timing")
-        return {"support_ms": float(ms[0]), "triangles_ms": float(ms[1]), "device_ms": float(ms[2])}
+        return {"support_ms": float(ms[0]), "delaunay_ms": float(ms[1]), "planes_ms": float(ms[2]),
+                "device_ms": float(ms[3])}
 
     def texel_bytes(self) -> int:
         """Bytes per source texel the NCC fetches read (2: binary16 copy, 4: fp32, 0: no views)."""

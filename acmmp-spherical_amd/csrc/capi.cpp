@@ -106,6 +106,10 @@ struct acmmp_ctx {
     bool has_result = false;          // planes_rm / costs_rm hold this problem's maps (a run, set_state[_device])
     char* d_pp = nullptr;             // planar-prior triangle tables (acmmp_set_planar_prior_from_maps)
     size_t pp_cap = 0;
+    char* h_pp = nullptr;             // their pinned host staging (upload_planar), reused once pp_ev has passed
+    size_t h_pp_cap = 0;
+    hipEvent_t pp_ev = nullptr;
+    bool pp_pending = false;
     int4* d_support = nullptr;        // support-point blocks (acmmp_set_planar_prior_from_state)
     size_t support_cap = 0;
 
@@ -117,7 +121,7 @@ struct acmmp_ctx {
     size_t scratch_bytes = 0;
 
     float timing[3] = {0.f, 0.f, 0.f};
-    float planar_ms[3] = {0.f, 0.f, 0.f};      // acmmp_last_planar_timing
+    float planar_ms[4] = {0.f, 0.f, 0.f, 0.f}; // acmmp_last_planar_timing
     std::vector<hipEvent_t> kev;              // 5 per half-sweep (per-kernel timing)
     float ktiming[4] = {0.f, 0.f, 0.f, 0.f};
     unsigned long long* d_work = nullptr;       // [256] k_eval_nb work counters + [256] the run's status word
@@ -168,6 +172,18 @@ hipError_t dreserve(T*& p, size_t& cap, size_t count) {
     const hipError_t e = dalloc(p, count);
     if (e == hipSuccess) cap = count;
     return e;
+}
+
+// Grow-only with headroom, for buffers whose size follows the problem's scale (the planar-prior tables and
+// support blocks): the next power of two of `count`, at least `min_count`, so a pipeline's scales reuse one
+// allocation -- a reallocation frees the old buffer, and hipFree waits for the whole device, other contexts'
+// kernels included.
+template <typename T>
+hipError_t dreserve_pow2(T*& p, size_t& cap, size_t count, size_t min_count) {
+    if (p && count <= cap) return hipSuccess;
+    size_t n = std::max<size_t>(min_count, 1);
+    while (n < count) n *= 2;
+    return dreserve(p, cap, n);
 }
 
 size_t P_of(const acmmp_ctx* c) { return static_cast<size_t>(c->W) * c->H; }
@@ -298,6 +314,8 @@ void acmmp_destroy(acmmp_ctx* c) {
         dfree(c->d_sel_cs[k]); dfree(c->d_rng_cs[k]);
     }
     for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
+    if (c->pp_ev) (void)hipEventDestroy(c->pp_ev);
+    if (c->h_pp) (void)hipHostFree(c->h_pp);
     for (auto& e : c->kev) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -798,17 +816,36 @@ static acmmp_status upload_planar(acmmp_ctx* c, const PlanarTriangles& pt, float
     const size_t o_row = up(o_step + n_step), n_row = sizeof(float2) * pt.row_trig.size();
     const size_t o_col = up(o_row + n_row), n_col = sizeof(float2) * pt.col_trig.size();
     const size_t bytes = up(o_col + n_col);
-    std::vector<char> host(bytes);
-    std::memcpy(host.data() + o_first, pt.first.data(), n_first);
-    if (n_plane) std::memcpy(host.data() + o_plane, pt.plane.data(), n_plane);
-    if (n_tri) std::memcpy(host.data() + o_tri, pt.tri.data(), n_tri);
-    if (n_step) std::memcpy(host.data() + o_step, pt.step.data(), n_step);
-    if (n_row) std::memcpy(host.data() + o_row, pt.row_trig.data(), n_row);
-    if (n_col) std::memcpy(host.data() + o_col, pt.col_trig.data(), n_col);
-    HIP_TRY(c, dreserve(c->d_pp, c->pp_cap, bytes));
+    // the tables go through a pinned staging buffer of the context, so the copy and the two kernels are only
+    // enqueued here: the next run_patchmatch on this stream follows them, acmmp_download_planar_prior waits for
+    // them, and the next call waits (pp_ev) before it rewrites the staging.  (Waiting here for the kernels put
+    // this call behind other contexts' RunPatchMatch kernels in the pipeline's overlapped planar passes: 83 of
+    // the stage's 206 ms at the bench scene, against 17 ms run alone -- profiles/r06_e2e_planar.json.)
+    if (c->pp_pending) {
+        HIP_TRY(c, hipEventSynchronize(c->pp_ev));
+        c->pp_pending = false;
+    }
+    if (!c->pp_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->pp_ev, hipEventDisableTiming));
+    if (bytes > c->h_pp_cap) {                               // (the same headroom as d_pp: hipHostFree syncs too)
+        if (c->h_pp) HIP_TRY(c, hipHostFree(c->h_pp));
+        c->h_pp = nullptr;
+        c->h_pp_cap = 0;
+        size_t n = static_cast<size_t>(16) << 20;
+        while (n < bytes) n *= 2;
+        HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_pp), n, hipHostMallocDefault));
+        c->h_pp_cap = n;
+    }
+    char* host = c->h_pp;
+    std::memcpy(host + o_first, pt.first.data(), n_first);
+    if (n_plane) std::memcpy(host + o_plane, pt.plane.data(), n_plane);
+    if (n_tri) std::memcpy(host + o_tri, pt.tri.data(), n_tri);
+    if (n_step) std::memcpy(host + o_step, pt.step.data(), n_step);
+    if (n_row) std::memcpy(host + o_row, pt.row_trig.data(), n_row);
+    if (n_col) std::memcpy(host + o_col, pt.col_trig.data(), n_col);
+    HIP_TRY(c, dreserve_pow2(c->d_pp, c->pp_cap, bytes, static_cast<size_t>(16) << 20));
     HIP_TRY(c, dreserve(c->d_prior, c->prior_cap, P));
     HIP_TRY(c, dreserve(c->d_mask, c->mask_cap, P));
-    HIP_TRY(c, hipMemcpyAsync(c->d_pp, host.data(), bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_pp, host, bytes, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemsetAsync(c->d_mask, 0, sizeof(uint32_t) * P, c->stream));
     PlanarDev pd;
     pd.first = reinterpret_cast<const long long*>(c->d_pp + o_first);
@@ -824,8 +861,9 @@ static acmmp_status upload_planar(acmmp_ctx* c, const PlanarTriangles& pt, float
     pd.depth_min = depth_min; pd.depth_max = depth_max;
     HIP_TRY(c, launch_planar_raster(pd, c->d_mask, c->stream));
     HIP_TRY(c, launch_planar_mask(pd, c->d_mask, c->d_prior, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));       // `host` is pageable and goes out of scope
-    c->planar_ms[2] = ms_since(t0);
+    HIP_TRY(c, hipEventRecord(c->pp_ev, c->stream));
+    c->pp_pending = true;
+    c->planar_ms[3] = ms_since(t0);
     c->has_prior = true;
     if (n_triangles) *n_triangles = m;
     return ACMMP_OK;
@@ -841,7 +879,8 @@ acmmp_status acmmp_set_planar_prior_from_maps(acmmp_ctx* c, const float* depths,
     const acmmp_status st = planar_triangles(c->cams[0], depths, costs, c->W, c->H, &pt);
     if (st != ACMMP_OK) return fail(c, st, "planar_triangles");
     c->planar_ms[0] = 0.f;                                  // the support-point scan is inside planar_triangles
-    c->planar_ms[1] = ms_since(t0);
+    c->planar_ms[1] = pt.delaunay_ms;
+    c->planar_ms[2] = ms_since(t0) - pt.delaunay_ms;
     return upload_planar(c, pt, depth_min, depth_max, n_triangles);
 }
 
@@ -854,7 +893,7 @@ acmmp_status acmmp_set_planar_prior_from_state(acmmp_ctx* c, float depth_min, fl
     const int W = c->W, H = c->H;
     const size_t nb = static_cast<size_t>((W + 4) / 5) * ((H + 4) / 5);
     const auto t0 = planar_clock::now();
-    HIP_TRY(c, dreserve(c->d_support, c->support_cap, nb));
+    HIP_TRY(c, dreserve_pow2(c->d_support, c->support_cap, nb, static_cast<size_t>(1) << 17));
     HIP_TRY(c, launch_support_points(c->d_costs_rm, c->d_planes_rm, W, H, c->d_support, c->stream));
     std::vector<int4> blocks(nb);
     HIP_TRY(c, hipMemcpyAsync(blocks.data(), c->d_support, sizeof(int4) * nb, hipMemcpyDeviceToHost, c->stream));
@@ -874,7 +913,8 @@ acmmp_status acmmp_set_planar_prior_from_state(acmmp_ctx* c, float depth_min, fl
     PlanarTriangles pt;
     const acmmp_status st = planar_triangles_pts(c->cams[0], xy, depth_at, W, H, &pt);
     if (st != ACMMP_OK) return fail(c, st, "planar_triangles");
-    c->planar_ms[1] = ms_since(t1);
+    c->planar_ms[1] = pt.delaunay_ms;
+    c->planar_ms[2] = ms_since(t1) - pt.delaunay_ms;
     return upload_planar(c, pt, depth_min, depth_max, n_triangles);
 }
 
@@ -882,6 +922,7 @@ acmmp_status acmmp_download_planar_prior(acmmp_ctx* c, float* prior, uint32_t* m
     if (!c) return ACMMP_ERR_INVALID_ARGUMENT;
     if (!c->has_prior) return fail(c, ACMMP_ERR_STATE, "no planar prior set since the last upload_views");
     HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));           // the raster / mask kernels upload_planar enqueued
     const size_t P = P_of(c);
     if (prior) HIP_TRY(c, d2h(prior, c->d_prior, sizeof(float4) * P));
     if (masks) HIP_TRY(c, d2h(masks, c->d_mask, sizeof(uint32_t) * P));
@@ -1375,9 +1416,9 @@ acmmp_status acmmp_last_timing(const acmmp_ctx* c, float ms[3]) {
     return ACMMP_OK;
 }
 
-acmmp_status acmmp_last_planar_timing(const acmmp_ctx* c, float ms[3]) {
+acmmp_status acmmp_last_planar_timing(const acmmp_ctx* c, float ms[4]) {
     if (!c || !ms) return ACMMP_ERR_INVALID_ARGUMENT;
-    for (int i = 0; i < 3; ++i) ms[i] = c->planar_ms[i];
+    for (int i = 0; i < 4; ++i) ms[i] = c->planar_ms[i];
     return ACMMP_OK;
 }
 

@@ -323,6 +323,49 @@ __device__ __forceinline__ void sphere_pixel_fast(Cam& c, f32x2 t, float tz, flo
 // fma order per row as three separate rows), with the pair of constants as one SGPR pair.
 // ft: the translation Ft, from the camera (nullptr) or from registers the caller holds (a VOP3 fma reads
 // one SGPR, so a translation in SGPRs costs a move per row and view-sample)
+// Two directions at once, their two atan polynomials as interleaved packed chains (a chain of dependent
+// v_pk_fma_f32 waits a hazard cycle between steps, s_nop; two chains fill each other's), the same operations per
+// direction as sphere_pixel_fast, so the same bits
+template <typename Cam>
+__device__ __forceinline__ void sphere_pixel_fast_x2(Cam& c, f32x2 ta, float tza, f32x2 tb, float tzb, float& oxa,
+                                                     float& oya, float& oxb, float& oyb) {
+    const float ha = __builtin_amdgcn_sqrtf(fmaf(tza, tza, ta.x * ta.x));
+    const float hb = __builtin_amdgcn_sqrtf(fmaf(tzb, tzb, tb.x * tb.x));
+    const f32x2 mna = (f32x2){min_abs(tza, ta.x), min_abs(ha, ta.y)};
+    const f32x2 mnb = (f32x2){min_abs(tzb, tb.x), min_abs(hb, tb.y)};
+    const f32x2 rca = (f32x2){__builtin_amdgcn_rcpf(max_abs(tza, ta.x)), __builtin_amdgcn_rcpf(max_abs(ha, ta.y))};
+    const f32x2 rcb = (f32x2){__builtin_amdgcn_rcpf(max_abs(tzb, tb.x)), __builtin_amdgcn_rcpf(max_abs(hb, tb.y))};
+    const f32x2 ua = mna * rca, ub = mnb * rcb;
+    const f32x2 za = ua * ua, zb = ub * ub;
+    f32x2 pa = splat2(-0.004355291370302439f), pb = pa;
+    pa = pk_fma(pa, za, splat2(0.023039722815155983f));
+    pb = pk_fma(pb, zb, splat2(0.023039722815155983f));
+    pa = pk_fma(pa, za, splat2(-0.05777300149202347f));
+    pb = pk_fma(pb, zb, splat2(-0.05777300149202347f));
+    pa = pk_fma(pa, za, splat2(0.09794192016124725f));
+    pb = pk_fma(pb, zb, splat2(0.09794192016124725f));
+    pa = pk_fma(pa, za, splat2(-0.139765664935112f));
+    pb = pk_fma(pb, zb, splat2(-0.139765664935112f));
+    pa = pk_fma(pa, za, splat2(0.19962701201438904f));
+    pb = pk_fma(pb, zb, splat2(0.19962701201438904f));
+    pa = pk_fma(pa, za, splat2(-0.3333165943622589f));
+    pb = pk_fma(pb, zb, splat2(-0.3333165943622589f));
+    f32x2 ra = pk_fma(ua * za, pa, ua);
+    f32x2 rb = pk_fma(ub * zb, pb, ub);
+    const f32x2 rqa = splat2(kPio2Hi) - ra, rqb = splat2(kPio2Hi) - rb;
+    ra.x = fabsf(ta.x) > fabsf(tza) ? rqa.x : ra.x;
+    rb.x = fabsf(tb.x) > fabsf(tzb) ? rqb.x : rb.x;
+    ra.y = fabsf(ta.y) > ha ? rqa.y : ra.y;
+    rb.y = fabsf(tb.y) > hb ? rqb.y : rb.y;
+    ra.x = __builtin_bit_cast(int, tza) < 0 ? kPiHi - ra.x : ra.x;
+    rb.x = __builtin_bit_cast(int, tzb) < 0 ? kPiHi - rb.x : rb.x;
+    const f32x2 anga = (f32x2){copysignf(ra.x, ta.x), copysignf(ra.y, ta.y)};
+    const f32x2 angb = (f32x2){copysignf(rb.x, tb.x), copysignf(rb.y, tb.y)};
+    const f32x2 oa = pk_fma(anga, (f32x2){c.fkx, c.fky}, (f32x2){c.cx, c.cy});
+    const f32x2 ob = pk_fma(angb, (f32x2){c.fkx, c.fky}, (f32x2){c.cx, c.cy});
+    oxa = oa.x; oya = oa.y; oxb = ob.x; oyb = ob.y;
+}
+
 template <int MODEL, typename Cam>
 __device__ __forceinline__ void project_fast(Cam& c, float3 P, float& ox, float& oy, const float* ft = nullptr) {
     const f32x2 fxy = ft ? (f32x2){ft[0], ft[1]} : (f32x2){c.Ft[0], c.Ft[1]};
@@ -690,6 +733,9 @@ constexpr uint32_t kFixNone = ~0u, kFixNan = ~0u - 1u;
 #ifndef ACMMP_NODE_HOMOG
 #define ACMMP_NODE_HOMOG 1
 #endif
+#ifndef ACMMP_NODE_PAIRS
+#define ACMMP_NODE_PAIRS 1
+#endif
 
 // The lane's index in its wave, read where it is used: an asm volatile statement is neither hoisted nor merged
 // with another read, so a value derived from it is not kept live from the prologue (k_eval_nb spilled its lane
@@ -952,6 +998,38 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
 #pragma unroll
                 for (int a = 0; a < 4; ++a) {
                     f32x2 nd[4];                            // (x - x00 unwrapped, y) per node of this column
+                    // node b of this column at source (x, y): x as the offset from the first node, unwrapped
+                    auto put_node = [&](int b, float x, float y) {
+                        if (a == 0 && b == 0) {
+                            x00 = x;
+                            nd[b].x = 0.0f;
+                        } else {
+                            const float dx = x - x00;
+                            nd[b].x = fmaf(-rintf(dx * c.invW), c.Wf, dx);
+                        }
+                        nd[b].y = y;
+                    };
+#if ACMMP_NODE_HOMOG && ACMMP_NODE_PAIRS
+                    // two nodes at a time: their atan polynomials interleave (a lone chain of dependent v_pk_fma_f32
+                    // waits a hazard cycle between steps: 929 s_nop in k_eval_nb<11,4,1,1>, 348 paired; the same
+                    // bits, scripts/ab_bitident.py)
+#pragma unroll
+                    for (int b = 0; b < 4; b += 2) {
+                        f32x2 hxy[2];
+                        float hz[2];
+#pragma unroll
+                        for (int k = 0; k < 2; ++k) {
+                            const float4 q = pt.rw[(kNode[a] * 6 + kNode[b + k]) * pt.stride];
+                            const float rwy = pt.rr[kNode[b + k] * pt.stride];
+                            hxy[k] = pk_fma(Mxy[2], splat2(q.y), pk_fma(Mxy[1], splat2(rwy), Mxy[0] * splat2(q.x)));
+                            hz[k] = fmaf(Mz[2], q.y, fmaf(Mz[1], rwy, Mz[0] * q.x));
+                        }
+                        float x0, y0, x1, y1;
+                        sphere_pixel_fast_x2(c, hxy[0], hz[0], hxy[1], hz[1], x0, y0, x1, y1);
+                        put_node(b, x0, y0);
+                        put_node(b + 1, x1, y1);
+                    }
+#else
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
                         const float4 q = pt.rw[(kNode[a] * 6 + kNode[b]) * pt.stride];
@@ -965,15 +1043,9 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         const float dep = depth_from_plane_fast(ph, rw);
                         project_fast<MODEL>(c, make_float3(rw.x * dep, rw.y * dep, rw.z * dep), x, y);
 #endif
-                        if (a == 0 && b == 0) {
-                            x00 = x;
-                            nd[b].x = 0.0f;
-                        } else {
-                            const float dx = x - x00;
-                            nd[b].x = fmaf(-rintf(dx * c.invW), c.Wf, dx);
-                        }
-                        nd[b].y = y;
+                        put_node(b, x, y);
                     }
+#endif
                     if (a == 0) {
                         x03 = nd[3].x;
                         y0max = fmaxf(nd[0].y, nd[3].y);
@@ -1934,11 +2006,13 @@ __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour
 // (round 5, profiles/r05_ab3_ab.txt): not kept.
 template <int MODEL, int VB, int TEX, int FM>
 #ifndef ACMMP_NB_SPH_WAVES
-// fast SPHERE: 6 waves (80 VGPRs, no spills).  Round 4's form (all 16 nodes of a view live at once) spilled 9 dwords at
+// fast SPHERE: 5 waves (92 VGPRs, no spills).  Round 4's form (all 16 nodes of a view live at once) spilled 9 dwords at
 // 7 waves and was 3% slower at 6; with the node-column form and no prologue values kept across the view loop
 // (ncc_chunk), 6 waves beat 7: k_eval_nb 1.545 -> 1.511 ms at the metric, C3 15.69 -> 15.30 ms
-// (profiles/r05_ab3_ab.txt)
-#define ACMMP_NB_SPH_WAVES 6
+// (profiles/r05_ab3_ab.txt).  Round 6's node pairs (sphere_pixel_fast_x2) hold two nodes' chains at once: 20 dwords
+// spilled at 6 waves (metric -1.2% against unpaired nodes), none at 5, where k_eval_nb takes 1.429 against 1.436 ms
+// unpaired at 6 (C3 13.62 / 13.78 ms; profiles/r06_ab5_pairs_ab.txt)
+#define ACMMP_NB_SPH_WAVES 5
 #endif
 __global__ __launch_bounds__(256, MODEL == kSphere ? (FM ? ACMMP_NB_SPH_WAVES : 8) : (FM ? 6 : 1)) void k_eval_nb(
     const KParams kp, const int colour) {
@@ -2806,6 +2880,34 @@ __global__ void k_merge(const KParams kp, const int do_post) {
     kp.sel_rm[center] = kp.sel_cs[colour][ci];
 }
 
+// Median of 21 values by a selection network where none is NaN or a zero: Batcher's odd-even merge sort on 32
+// wires with 11 padded by +inf, cut to the 91 compare-exchanges that reach output 10 and to the min / max halves
+// that are read (162 v_min / v_max; scripts/median_net.py generates and checks it).  Without NaNs and signed
+// zeros any selection returns the median's bits, so this equals the insertion sort's d[10] (ACMMP.cu:1388-1401).
+// Entries {a, b, m}: m & 1 keeps min(v[a], v[b]) in v[a], m & 2 keeps the max in v[b].
+__constant__ constexpr unsigned char kMed21[91][3] = {
+    {0, 1, 3}, {2, 3, 3}, {0, 2, 3}, {1, 3, 3}, {1, 2, 3}, {4, 5, 3}, {6, 7, 3}, {4, 6, 3}, {5, 7, 3}, {5, 6, 3},
+    {0, 4, 3}, {2, 6, 3}, {2, 4, 3}, {1, 5, 3}, {3, 7, 3}, {3, 5, 3}, {1, 2, 3}, {3, 4, 3}, {5, 6, 3}, {8, 9, 3},
+    {10, 11, 3}, {8, 10, 3}, {9, 11, 3}, {9, 10, 3}, {12, 13, 3}, {14, 15, 3}, {12, 14, 3}, {13, 15, 3},
+    {13, 14, 3}, {8, 12, 3}, {10, 14, 3}, {10, 12, 3}, {9, 13, 3}, {11, 15, 3}, {11, 13, 3}, {9, 10, 3},
+    {11, 12, 3}, {13, 14, 3}, {0, 8, 3}, {4, 12, 3}, {4, 8, 3}, {2, 10, 3}, {6, 14, 1}, {6, 10, 3}, {2, 4, 3},
+    {6, 8, 3}, {10, 12, 3}, {1, 9, 3}, {5, 13, 3}, {5, 9, 3}, {3, 11, 3}, {7, 15, 1}, {7, 11, 3}, {3, 5, 3},
+    {7, 9, 3}, {11, 13, 1}, {1, 2, 3}, {3, 4, 3}, {5, 6, 3}, {7, 8, 3}, {9, 10, 3}, {11, 12, 3}, {16, 17, 3},
+    {18, 19, 3}, {16, 18, 3}, {17, 19, 3}, {17, 18, 3}, {16, 20, 3}, {18, 20, 3}, {17, 18, 3}, {19, 20, 3},
+    {18, 20, 3}, {17, 18, 3}, {19, 20, 3}, {0, 16, 2}, {8, 16, 2}, {4, 20, 2}, {12, 20, 1}, {12, 16, 1},
+    {2, 18, 2}, {10, 18, 1}, {6, 10, 2}, {10, 12, 1}, {1, 17, 2}, {9, 17, 1}, {5, 9, 2}, {3, 19, 2}, {11, 19, 1},
+    {7, 11, 1}, {7, 9, 2}, {9, 10, 2}};
+__device__ __forceinline__ float median21(float (&v)[21]) {
+#pragma unroll
+    for (int k = 0; k < 91; ++k) {
+        const int a = kMed21[k][0], b = kMed21[k][1], m = kMed21[k][2];
+        const float lo = fminf(v[a], v[b]), hi = fmaxf(v[a], v[b]);
+        if (m & 1) v[a] = lo;
+        if (m & 2) v[b] = hi;
+    }
+    return v[10];
+}
+
 // CheckerboardFilter, ACMMP.cu:1366-1480 (in place; reads only the other colour)
 #if ACMMP_IN_TU(0)
 __global__ void k_filter(const KParams kp, const int colour) {
@@ -2828,6 +2930,13 @@ __global__ void k_filter(const KParams kp, const int colour) {
                        wv(center + 1), wv(center + 3), wv(center + 5), wv(center - w + 2), wv(center + w + 2),
                        wv(center - w - 2), wv(center + w - 2), wv(center - 1 - 2 * w), wv(center + 1 - 2 * w),
                        wv(center - 1 + 2 * w), wv(center + 1 + 2 * w)};
+        bool plain = true;                                   // no NaN, no signed zero among the taps
+#pragma unroll
+        for (int i = 0; i < 21; ++i) plain = plain && d[i] == d[i] && d[i] != 0.0f;
+        if (plain) {
+            kp.planes_rm[center].w = median21(d);
+            return;
+        }
 #pragma unroll
         for (int i = 1; i < 21; ++i) {
             const float tmp = d[i];
@@ -3229,11 +3338,17 @@ hipError_t launch_eval_ref(const KParams& kp0, int colour, hipStream_t s) {
     if (ref_fix) k_nb_fix<1, true><<<16 * kNbFixRegions, 256, 0, s>>>(kp, colour);
     if (kp.ref_split > 0) {
         // the survivors' prefix over k_eval_ref blocks, then 8 x nk tail blocks (the queue's length is
-        // known on the device only: nk covers the largest possible queue, up to 256 blocks per XCD)
+        // known on the device only: nk covers the largest possible queue, up to ACMMP_TAIL_NK blocks per XCD; blocks
+        // past the queue's end return at once).  Round 5 capped nk at 256: 8192 waves for the metric's ~640k
+        // survivors, so most waves took a second, mostly idle pass over the grid-stride loop (the tail's VALU count
+        // was 2.4x one pass's).
+#ifndef ACMMP_TAIL_NK
+#define ACMMP_TAIL_NK 2048
+#endif
         const int nref = static_cast<int>(grd_ref.x);
         k_tail_scan<<<1, 1024, 0, s>>>(kp, nref);
         k_tail_compact<<<static_cast<unsigned>(nref), 256, 0, s>>>(kp);
-        const unsigned grd = 8u * static_cast<unsigned>(std::min<long long>(256, std::max<long long>(1, cdiv(static_cast<long long>(nref) * kRefSlots, 8 * 256))));
+        const unsigned grd = 8u * static_cast<unsigned>(std::min<long long>(ACMMP_TAIL_NK, std::max<long long>(1, cdiv(static_cast<long long>(nref) * kRefSlots, 8 * 256))));
         if (kp.geom) ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, true, TF><<<grd, 256, 0, s>>>(kp, colour, nref))));
         else ACMMP_DISPATCH_TF(kp, ACMMP_DISPATCH(kp.model, kp.V, (k_eval_ref_tail<M, VBC, false, TF><<<grd, 256, 0, s>>>(kp, colour, nref))));
     }

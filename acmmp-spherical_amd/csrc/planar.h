@@ -21,6 +21,7 @@ struct PlanarTriangles {
     std::vector<long long> first;  // exclusive prefix of the p-steps per triangle (size n + 1)
     std::vector<float2> row_trig;  // SPHERE: (sin, cos) of each row's latitude, host libm (H)
     std::vector<float2> col_trig;  // SPHERE: (sin, cos) of each column's longitude (W)
+    float delaunay_ms = 0.f;       // host wall time of the triangulation (acmmp_last_planar_timing)
 };
 
 // Host half: support points of `costs`, Delaunay, labelled triangles, their planes through `depths`.

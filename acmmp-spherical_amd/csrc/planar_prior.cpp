@@ -14,11 +14,16 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <thread>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <cstdlib>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "acmmp.h"
@@ -62,6 +67,82 @@ struct Tri {
     int v[3];     // counter-clockwise
     int nb[3];    // neighbour across the edge opposite v[i]; -1 = none
     bool alive;
+};
+
+// Host worker threads shared by every planar-prior call of the process: run(n, f) calls f(0 .. n-1) on the
+// pool's workers and the calling thread and returns when all have returned.  A call spawned ~100 std::threads
+// (the Delaunay strips, the merges' halves, the triangle scan, the plane fits) -- milliseconds of thread creation
+// per call, with three pipeline contexts calling at once.  The caller takes its own job's tasks too, so a task
+// may call run() itself (the merges nest) without waiting on a busy pool.
+class HostPool {
+public:
+    static HostPool& get() {
+        static HostPool* p = new HostPool();               // never destroyed: the workers outlive static destructors
+        return *p;
+    }
+    template <typename F>
+    void run(int n, F&& f) {
+        if (n <= 1 || workers_ == 0) {
+            for (int t = 0; t < n; ++t) f(t);
+            return;
+        }
+        Job job;
+        job.n = n;
+        job.fn = [&f](int t) { f(t); };
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            jobs_.push_back(&job);
+        }
+        cv_.notify_all();
+        for (int t; (t = job.next.fetch_add(1)) < n;) {
+            job.fn(t);
+            job.done.fetch_add(1);
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &job));
+        }
+        while (job.done.load() < n) std::this_thread::yield();   // workers finishing this job's last tasks
+    }
+    int threads() const { return workers_ + 1; }
+
+private:
+    struct Job {
+        int n = 0;
+        std::function<void(int)> fn;
+        std::atomic<int> next{0}, done{0};
+    };
+    HostPool() {
+        const unsigned hw = std::thread::hardware_concurrency();
+        workers_ = static_cast<int>(std::min<unsigned>(hw ? hw : 1, 16u)) - 1;
+        for (int k = 0; k < workers_; ++k) std::thread([this] { work(); }).detach();
+    }
+    void work() {
+        for (;;) {
+            Job* j = nullptr;
+            int t = 0;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] {
+                    for (Job* x : jobs_)
+                        if (x->next.load() < x->n) return true;
+                    return false;
+                });
+                for (Job* x : jobs_) {
+                    t = x->next.fetch_add(1);
+                    if (t < x->n) { j = x; break; }
+                }
+            }
+            if (j) {
+                j->fn(t);
+                j->done.fetch_add(1);
+            }
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<Job*> jobs_;
+    int workers_ = 0;
 };
 
 class Delaunay {
@@ -264,9 +345,26 @@ private:
 // be the incremental one's (neither is cv::Subdiv2D's), and it does not depend on the thread
 // count (the strips and split points are fixed by n).  The Hilbert-order incremental insertion stays the
 // fallback (duplicate points, fewer than 3 points per strip, edge-pool overflow).
+// The quad-edge arrays of one triangulation, kept between calls (DelaunayDC takes one from this pool and gives it
+// back): fresh ones were ~10 MB of first-touch page faults per 68k-point call, 6 of its 57 ms on one host thread.
+struct DcWorkspace {
+    std::vector<int> onext, org, order;
+    std::vector<unsigned char> alive;
+};
+std::mutex g_dc_mu;
+std::vector<std::unique_ptr<DcWorkspace>> g_dc_free;
+
 class DelaunayDC {
 public:
-    explicit DelaunayDC(const std::vector<Pt>& pts) : p_(pts), n_(static_cast<int>(pts.size())) {}
+    explicit DelaunayDC(const std::vector<Pt>& pts)
+        : p_(pts), n_(static_cast<int>(pts.size())), ws_(take_ws()), onext_(ws_->onext), org_(ws_->org),
+          order_(ws_->order), alive_(ws_->alive) {}
+    ~DelaunayDC() {
+        std::lock_guard<std::mutex> g(g_dc_mu);
+        if (g_dc_free.size() < 8) g_dc_free.push_back(std::move(ws_));
+    }
+    DelaunayDC(const DelaunayDC&) = delete;
+    DelaunayDC& operator=(const DelaunayDC&) = delete;
 
     // false: the incremental form must do it (duplicate points, degenerate strips, edge pool exhausted)
     bool run() {
@@ -314,9 +412,10 @@ public:
         merge_base_ = base;
         next_.store(base);
         cap_ = base + 3 * static_cast<size_t>(n_) + 1024;
-        onext_.resize(4 * cap_);
-        org_.resize(2 * cap_);
-        alive_.assign(cap_, 0);
+        if (onext_.size() < 4 * cap_) onext_.resize(4 * cap_);   // (written before read: no clearing)
+        if (org_.size() < 2 * cap_) org_.resize(2 * cap_);
+        if (alive_.size() < cap_) alive_.resize(cap_);
+        std::fill(alive_.begin(), alive_.begin() + static_cast<std::ptrdiff_t>(cap_), static_cast<unsigned char>(0));
         auto strip_task = [&](int t) {
             for (int k = t; k < S; k += T) {
                 const int lo = strip_lo_[k], hi = strip_lo_[k + 1];
@@ -327,12 +426,7 @@ public:
                 strips_[k] = r.le < 0 ? EdgePair{-1, -1} : to_x_frame(r.le);
             }
         };
-        {
-            std::vector<std::thread> th;
-            for (int t = 1; t < T; ++t) th.emplace_back(strip_task, t);
-            strip_task(0);
-            for (auto& x : th) x.join();
-        }
+        HostPool::get().run(T, strip_task);
         for (TaskPool& tp : pool_) tp.bump = tp.end = 0;        // the merges allocate through next_
         for (const EdgePair& e : strips_)
             if (e.le < 0) return false;
@@ -345,14 +439,25 @@ public:
     }
 
     std::vector<std::array<int, 3>> triangles() const {
-        // every face bounded by three edges and turning left: one triangle, kept from the directed edge leaving
-        // its lowest point index; the quads scanned in parallel ranges
-        std::vector<int> start(static_cast<size_t>(n_) + 1, 0);
+        // every face bounded by three edges and turning left: one triangle, kept from the directed edge leaving its
+        // lowest point index a, in (a, b, c) order.  The live quads are scanned in parallel ranges; each triangle is
+        // counted into its point a's bucket (atomics), the buckets' prefix taken, every triangle placed into its
+        // bucket (atomic cursors, so any order within a bucket) and each bucket sorted -- in parallel throughout
+        // (round 5 concatenated the ranges' lists and bucketed them with one serial counting sort: 15 of the 57 ms
+        // of a 68k-point call on one host thread; walking each point's edge ring instead had the scan's locality
+        // lost, +20 ms on one thread)
         const size_t used = std::min(next_.load(), cap_);      // (the strip ranges lie below merge_base_)
         const unsigned hw = std::thread::hardware_concurrency();
         const int T = used > 65536 ? static_cast<int>(std::min<unsigned>(hw ? hw : 1, 16u)) : 1;
+        auto run_on = [&](auto&& f) { HostPool::get().run(T, f); };
+        auto lo = [&](int t) { return static_cast<int>(static_cast<long long>(n_) * t / T); };
         std::vector<std::vector<std::array<int, 3>>> part(T);
-        auto scan = [&](int t) {
+        std::unique_ptr<std::atomic<int>[]> cnt(new std::atomic<int>[static_cast<size_t>(n_) + 1]);
+        run_on([&](int t) {
+            for (int a = lo(t); a < lo(t + 1); ++a) cnt[a + 1].store(0, std::memory_order_relaxed);
+            if (t == 0) cnt[0].store(0, std::memory_order_relaxed);
+        });
+        run_on([&](int t) {
             std::vector<std::array<int, 3>>& out = part[t];
             out.reserve(used / T + 16);
             for (size_t q = used * t / T; q < used * (t + 1) / T; ++q) {
@@ -365,24 +470,24 @@ public:
                     if (!(a < c) || lnext(e2) != e) continue;
                     if (orient(p_[a], p_[b], p_[c]) <= 0) continue;
                     out.push_back({a, b, c});
+                    cnt[a + 1].fetch_add(1, std::memory_order_relaxed);
                 }
             }
-        };
-        {
-            std::vector<std::thread> th;
-            for (int t = 1; t < T; ++t) th.emplace_back(scan, t);
-            scan(0);
-            for (auto& x : th) x.join();
-        }
-        std::vector<std::array<int, 3>> tris;
-        for (auto& v : part) tris.insert(tris.end(), v.begin(), v.end());
-        for (const auto& t : tris) ++start[t[0] + 1];
-        for (int i = 0; i < n_; ++i) start[i + 1] += start[i];
-        std::vector<std::array<int, 3>> out(tris.size());
-        std::vector<int> fill(start.begin(), start.end() - 1);
-        for (const auto& t : tris) out[fill[t[0]]++] = t;
-        for (int i = 0; i < n_; ++i)
-            if (start[i + 1] - start[i] > 1) std::sort(out.begin() + start[i], out.begin() + start[i + 1]);
+        });
+        std::vector<int> start(static_cast<size_t>(n_) + 1);
+        start[0] = 0;
+        for (int i = 0; i < n_; ++i) start[i + 1] = start[i] + cnt[i + 1].load(std::memory_order_relaxed);
+        run_on([&](int t) {                                    // the cursors: each bucket's start
+            for (int a = lo(t); a < lo(t + 1); ++a) cnt[a].store(start[a], std::memory_order_relaxed);
+        });
+        std::vector<std::array<int, 3>> out(static_cast<size_t>(start[n_]));
+        run_on([&](int t) {
+            for (const auto& tr : part[t]) out[cnt[tr[0]].fetch_add(1, std::memory_order_relaxed)] = tr;
+        });
+        run_on([&](int t) {
+            for (int a = lo(t); a < lo(t + 1); ++a)
+                if (start[a + 1] - start[a] > 1) std::sort(out.begin() + start[a], out.begin() + start[a + 1]);
+        });
         return out;
     }
 
@@ -490,9 +595,10 @@ private:
         if (depth < par_levels_) {
             // the right half on its own thread (free list tid_r), the left half on this one
             const int tid_r = tid + (1 << (par_levels_ - 1 - depth));
-            std::thread th([&] { R = merge_strips(mid, s1, depth + 1, tid_r); });
-            L = merge_strips(s0, mid, depth + 1, tid);
-            th.join();
+            HostPool::get().run(2, [&](int h) {
+                if (h == 0) L = merge_strips(s0, mid, depth + 1, tid);
+                else R = merge_strips(mid, s1, depth + 1, tid_r);
+            });
             pool_[tid].free.insert(pool_[tid].free.end(), pool_[tid_r].free.begin(), pool_[tid_r].free.end());
             pool_[tid_r].free.clear();
         } else {
@@ -543,12 +649,23 @@ private:
         return {ldo, rdo};
     }
 
+    static std::unique_ptr<DcWorkspace> take_ws() {
+        std::lock_guard<std::mutex> g(g_dc_mu);
+        if (g_dc_free.empty()) return std::make_unique<DcWorkspace>();
+        std::unique_ptr<DcWorkspace> w = std::move(g_dc_free.back());
+        g_dc_free.pop_back();
+        return w;
+    }
     const std::vector<Pt>& p_;
     int n_;
+    std::unique_ptr<DcWorkspace> ws_;
+    std::vector<int>& onext_;
+    std::vector<int>& org_;
+    std::vector<int>& order_;
+    std::vector<unsigned char>& alive_;
     size_t cap_ = 0;
-    std::vector<int> onext_, org_, order_, strip_lo_;
+    std::vector<int> strip_lo_;
     std::vector<EdgePair> strips_;
-    std::vector<unsigned char> alive_;
     std::atomic<size_t> next_{0};
     std::atomic<bool> overflow_{false};
     // per task: its free quads and its pool range, each on its own cache lines (adjacent, every make_edge of one
@@ -610,10 +727,7 @@ void parallel_for(int n, F&& f) {
             for (int i = b; i < e; ++i) f(i);
         }
     };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(worker);
-    worker();
-    for (auto& t : th) t.join();
+    HostPool::get().run(nt, [&](int) { worker(); });
 }
 
 // GetSupportPoints (ACMMP.cpp:904-929): per 5x5 block in column-major block order, the first
@@ -665,9 +779,31 @@ float sphere_depth(const float plane[4], SphereTrig lat, SphereTrig lon) {
 }
 
 // GetPriorPlaneParams (ACMMP.cpp:957-989) through the three vertices' depths d3
+// GetPriorPlaneParams on the points X[3] (Get3DPointonRefCam of the triangle's vertices)
+void plane_through(float X[3][3], float plane[4]);
+
 void prior_plane(const acmmp_camera& cam, const int tri_xy[6], const float d3[3], float plane[4]) {
     float X[3][3];
     for (int k = 0; k < 3; ++k) point_on_ref_cam(tri_xy[2 * k], tri_xy[2 * k + 1], d3[k], cam, X[k]);
+    plane_through(X, plane);
+}
+
+// The same with a SPHERE camera's (sin, cos) of each row's latitude and each column's longitude from tables
+// (sphere_row / sphere_col: the values point_on_ref_cam computes, so the same bits) instead of four libm calls
+// per vertex -- those were most of the host half's plane fits (136k triangles at 2000x1500)
+void prior_plane_trig(const int tri_xy[6], const float d3[3], const float2* row_trig, const float2* col_trig,
+                      float plane[4]) {
+    float X[3][3];
+    for (int k = 0; k < 3; ++k) {
+        const float2 lon = col_trig[tri_xy[2 * k]], lat = row_trig[tri_xy[2 * k + 1]];
+        X[k][0] = lat.y * lon.x * d3[k];
+        X[k][1] = -lat.x * d3[k];
+        X[k][2] = lat.y * lon.y * d3[k];
+    }
+    plane_through(X, plane);
+}
+
+void plane_through(float X[3][3], float plane[4]) {
 
     // cv::SVD::solveZ on [X_k 1] (3x4): the null vector, i.e. the plane through the three points
     // (ACMMP.cpp:960-980).  Closed form: n = (X2-X1) x (X3-X1), w = -n.X1.
@@ -676,7 +812,9 @@ void prior_plane(const acmmp_camera& cam, const int tri_xy[6], const float d3[3]
     float n4[4] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0], 0.f};
     n4[3] = -(n4[0] * X[0][0] + n4[1] * X[0][1] + n4[2] * X[0][2]);
     // ACMMP.cpp:981-988: normalise by the normal's length, sign so that w >= 0
-    float norm2 = static_cast<float>(std::sqrt(std::pow(n4[0], 2) + std::pow(n4[1], 2) + std::pow(n4[2], 2)));
+    // std::pow(float, 2) is the double pow of the promoted value: its square, exact in double
+    const double nx = n4[0], ny = n4[1], nz = n4[2];
+    float norm2 = static_cast<float>(std::sqrt(nx * nx + ny * ny + nz * nz));
     if (n4[3] < 0) norm2 *= -1;
     for (int k = 0; k < 4; ++k) plane[k] = n4[k] / norm2;
 }
@@ -808,20 +946,38 @@ acmmp_status planar_triangles_pts(const acmmp_camera& cam, const std::vector<int
                                   const std::vector<float>& depth_at, int W, int H, PlanarTriangles* out) {
     const int n = static_cast<int>(xy.size() / 2);
     std::vector<int> tri, tri_pt;                          // vertex coordinates / point indices
+    const auto t0 = std::chrono::steady_clock::now();
     if (n > 0) {                                           // triangulate once (ACMMP.cpp:932-955)
         std::vector<Pt> pts(n);
         for (int i = 0; i < n; ++i) pts[i] = {xy[2 * i], xy[2 * i + 1]};
-        for (const auto& t : delaunay_triangles(pts, std::max<long long>(std::max(W, H), 1))) {
-            bool inside = true;
-            for (int j = 0; j < 3; ++j) {
-                const int x = xy[2 * t[j]], y = xy[2 * t[j] + 1];
-                inside = inside && x >= 0 && x < W && y >= 0 && y < H;
-            }
-            if (!inside) continue;
-            for (int j = 0; j < 3; ++j) {
-                tri.push_back(xy[2 * t[j]]);
-                tri.push_back(xy[2 * t[j] + 1]);
-                tri_pt.push_back(t[j]);
+        const auto dt = delaunay_triangles(pts, std::max<long long>(std::max(W, H), 1));
+        out->delaunay_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        bool all_inside = true;                             // (support points always are: then no triangle drops out)
+        for (int i = 0; i < n && all_inside; ++i)
+            all_inside = xy[2 * i] >= 0 && xy[2 * i] < W && xy[2 * i + 1] >= 0 && xy[2 * i + 1] < H;
+        if (all_inside) {
+            tri.resize(6 * dt.size());
+            tri_pt.resize(3 * dt.size());
+            parallel_for(static_cast<int>(dt.size()), [&](int k) {
+                for (int j = 0; j < 3; ++j) {
+                    tri[6 * static_cast<size_t>(k) + 2 * j] = xy[2 * dt[k][j]];
+                    tri[6 * static_cast<size_t>(k) + 2 * j + 1] = xy[2 * dt[k][j] + 1];
+                    tri_pt[3 * static_cast<size_t>(k) + j] = dt[k][j];
+                }
+            });
+        } else {
+            for (const auto& t : dt) {
+                bool inside = true;
+                for (int j = 0; j < 3; ++j) {
+                    const int x = xy[2 * t[j]], y = xy[2 * t[j] + 1];
+                    inside = inside && x >= 0 && x < W && y >= 0 && y < H;
+                }
+                if (!inside) continue;
+                for (int j = 0; j < 3; ++j) {
+                    tri.push_back(xy[2 * t[j]]);
+                    tri.push_back(xy[2 * t[j] + 1]);
+                    tri_pt.push_back(t[j]);
+                }
             }
         }
     }
@@ -829,12 +985,23 @@ acmmp_status planar_triangles_pts(const acmmp_camera& cam, const std::vector<int
     out->tri = std::move(tri);
     out->plane.assign(4 * static_cast<size_t>(m), 0.f);
     out->step.assign(m, 0.f);
+    out->row_trig.clear();
+    out->col_trig.clear();
+    const bool sphere = cam.model == ACMMP_SPHERE;
+    if (sphere) {
+        out->row_trig.resize(H);
+        out->col_trig.resize(W);
+        for (int y = 0; y < H; ++y) { const SphereTrig r = sphere_row(cam, y); out->row_trig[y] = make_float2(r.s, r.c); }
+        for (int x = 0; x < W; ++x) { const SphereTrig k = sphere_col(cam, x); out->col_trig[x] = make_float2(k.s, k.c); }
+    }
     std::vector<long long> np(m, 0);
     parallel_for(m, [&](int k) {
         const int* t = &out->tri[6 * static_cast<size_t>(k)];
-        const float L01 = static_cast<float>(std::sqrt(std::pow(t[0] - t[2], 2) + std::pow(t[1] - t[3], 2)));
-        const float L02 = static_cast<float>(std::sqrt(std::pow(t[0] - t[4], 2) + std::pow(t[1] - t[5], 2)));
-        const float L12 = static_cast<float>(std::sqrt(std::pow(t[2] - t[4], 2) + std::pow(t[3] - t[5], 2)));
+        // main.cpp:146-148's sqrt(pow(d, 2) + ...) in double: pow(d, 2) of an integer d is d * d exactly
+        auto sq = [](int d) { return static_cast<double>(d) * static_cast<double>(d); };
+        const float L01 = static_cast<float>(std::sqrt(sq(t[0] - t[2]) + sq(t[1] - t[3])));
+        const float L02 = static_cast<float>(std::sqrt(sq(t[0] - t[4]) + sq(t[1] - t[5])));
+        const float L12 = static_cast<float>(std::sqrt(sq(t[2] - t[4]) + sq(t[3] - t[5])));
         const float max_edge_length = std::max(L01, std::max(L02, L12));
         const float step = static_cast<float>(1.0 / max_edge_length);
         out->step[k] = step;
@@ -842,18 +1009,11 @@ acmmp_status planar_triangles_pts(const acmmp_camera& cam, const std::vector<int
         for (float p = 0; p < 1.0; p += step) ++c;
         np[k] = c;
         const float d3[3] = {depth_at[tri_pt[3 * k]], depth_at[tri_pt[3 * k + 1]], depth_at[tri_pt[3 * k + 2]]};
-        prior_plane(cam, t, d3, &out->plane[4 * static_cast<size_t>(k)]);
+        if (sphere) prior_plane_trig(t, d3, out->row_trig.data(), out->col_trig.data(), &out->plane[4 * static_cast<size_t>(k)]);
+        else prior_plane(cam, t, d3, &out->plane[4 * static_cast<size_t>(k)]);
     });
     out->first.assign(static_cast<size_t>(m) + 1, 0);
     for (int k = 0; k < m; ++k) out->first[k + 1] = out->first[k] + np[k];
-    out->row_trig.clear();
-    out->col_trig.clear();
-    if (cam.model == ACMMP_SPHERE) {
-        out->row_trig.resize(H);
-        out->col_trig.resize(W);
-        for (int y = 0; y < H; ++y) { const SphereTrig r = sphere_row(cam, y); out->row_trig[y] = make_float2(r.s, r.c); }
-        for (int x = 0; x < W; ++x) { const SphereTrig k = sphere_col(cam, x); out->col_trig[x] = make_float2(k.s, k.c); }
-    }
     return ACMMP_OK;
 }
 

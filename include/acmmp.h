@@ -214,10 +214,12 @@ acmmp_status acmmp_last_kernel_timing(const acmmp_ctx *ctx, float ms[4], int lau
 acmmp_status acmmp_last_work(const acmmp_ctx *ctx, unsigned long long *evaluated, unsigned long long *total);
 
 /* Host wall-clock breakdown of the last acmmp_set_planar_prior_from_state / _from_maps call, in ms:
- * [support points (device kernel + copy back, or host scan), triangles (Delaunay, plane fits and step
- * tables on the host), device half (table upload, raster and mask kernels, until they complete)].
+ * [support points (device kernel + copy back; 0 for _from_maps, whose host scan is in the next entry),
+ * Delaunay triangulation (host), the rest of the host half (labelled triangles, plane fits, step and trig
+ * tables), device half (staging and enqueueing the table upload and the raster and mask kernels on the
+ * context's stream -- they complete before its next run; see acmmp_set_planar_prior_from_maps)].
  * No reference counterpart (profiling of main.cpp:113-187's block). */
-acmmp_status acmmp_last_planar_timing(const acmmp_ctx *ctx, float ms[3]);
+acmmp_status acmmp_last_planar_timing(const acmmp_ctx *ctx, float ms[4]);
 
 /* Bytes per source texel the NCC fetches read: 2 when every texel of the uploaded views is exactly
  * a binary16 number (8-bit images are) and the engine keeps a binary16 copy of them, 4 for the fp32
@@ -372,7 +374,8 @@ acmmp_status acmmp_set_planar_prior_from_maps(acmmp_ctx *ctx, const float *depth
  * support points (and their depths) to the host for the Delaunay triangulation and the per-triangle planes,
  * then the raster / mask / expansion of acmmp_set_planar_prior_from_maps.  Equal to
  * acmmp_set_planar_prior_from_maps on the downloaded maps, bit for bit (tests/test_gpu_planar_state.py);
- * no full-map download. */
+ * no full-map download.  Both calls return once the raster and mask kernels are enqueued on the context's
+ * stream (its next RunPatchMatch runs after them; acmmp_download_planar_prior waits for them). */
 acmmp_status acmmp_set_planar_prior_from_state(acmmp_ctx *ctx, float depth_min, float depth_max, int *n_triangles);
 /* Test hook: the planar-prior state of the context (P float4 planes, P labels; either may be NULL). */
 acmmp_status acmmp_download_planar_prior(acmmp_ctx *ctx, float *prior_planes, uint32_t *masks);

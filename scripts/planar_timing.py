@@ -41,9 +41,19 @@ for _ in range(3):
     t = time.perf_counter(); ctx.set_planar_prior_from_maps(depth, costs, float(p["depth_min"]), float(p["depth_max"]))
     ts.append((time.perf_counter() - t) * 1e3)
 out["set_planar_prior_from_maps_ms"] = ts
-ts = []
+ts, parts = [], []
 for _ in range(3):
     t = time.perf_counter(); out["n_tri_state"] = ctx.set_planar_prior_from_state(float(p["depth_min"]), float(p["depth_max"]))
     ts.append((time.perf_counter() - t) * 1e3)
+    parts.append(ctx.last_planar_timing())
 out["set_planar_prior_from_state_ms"] = ts
+out["set_planar_prior_from_state_parts"] = parts
+# the host Delaunay alone (the triangles part's bulk) by thread count
+for nt in (1, 4, 8, 16):
+    os.environ["ACMMP_DELAUNAY_THREADS"] = str(nt)
+    best = 1e9
+    for _ in range(3):
+        t = time.perf_counter(); capi.delaunay(xy, W, H); best = min(best, (time.perf_counter() - t) * 1e3)
+    out[f"delaunay_ms_threads{nt}"] = best
+del os.environ["ACMMP_DELAUNAY_THREADS"]
 print(json.dumps(out))

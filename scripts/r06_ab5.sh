@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 6: bit-identity of two builds (scripts/ab_bitident.py), then alternated bench lines of variants, then the
+# product's planar-prior timing and end-to-end line.  Usage: bash scripts/r06_ab5.sh TAG BASE CAND "LIBS" "CONFIG1" ...
+set -o pipefail
+export TMPDIR=/tmp
+TAG=$1; BASE=$2; CAND=$3; LIBS=$4; shift 4
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+ACMMP_LIB=$BASE timeout -k 10 300 python scripts/ab_bitident.py run $OUT/base.npz > $OUT/bit.log 2>&1 || { tail $OUT/bit.log; exit 1; }
+ACMMP_LIB=$CAND timeout -k 10 300 python scripts/ab_bitident.py run $OUT/cand.npz >> $OUT/bit.log 2>&1 || { tail $OUT/bit.log; exit 1; }
+python scripts/ab_bitident.py cmp $OUT/base.npz $OUT/cand.npz | tail -9
+rm -f $OUT/base.npz $OUT/cand.npz
+for cfg in "$@"; do
+  for rep in 1 2; do
+    for lib in $LIBS; do
+      ACMMP_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-variant --no-pipeline --no-other-mode $cfg > $OUT/b.json 2> $OUT/b.err || { tail $OUT/b.err; exit 1; }
+      python -c "import json,os;d=json.load(open('$OUT/b.json'));print(os.path.basename('$lib'), '$cfg', d['value'], d['ms_per_step'], d['clock']['ghz'], d['roofline']['half_sweep_kernels_ms'])" | tee -a $OUT/ab.txt
+    done
+  done
+done
+timeout -k 10 200 python scripts/planar_timing.py 2000 1500 sphere > $OUT/planar_sphere.json || exit 1
+timeout -k 10 400 python bench.py --no-cpu-baseline --no-variant --no-other-mode > $OUT/bench.json 2> $OUT/bench.err || exit 1
+python -c "import json;d=json.load(open('$OUT/bench.json'));print(d['value'], json.dumps(d['end_to_end']['stages_s']))"
+echo AB_DONE

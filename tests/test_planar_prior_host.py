@@ -168,10 +168,17 @@ def np_raster(tri, W, H, label, mask):
         p = f32(p + step)
 
 
-def test_planar_prior_host_pipeline_matches_restatement():
+@pytest.mark.parametrize("model", [types.PINHOLE, types.SPHERE])
+def test_planar_prior_host_pipeline_matches_restatement(model):
+    # (SPHERE: the host half fits its planes with the row / column trig tables, prior_plane_params with libm per
+    # vertex -- the same bits)
     W, H = 90, 60
-    cam = types.make_camera(types.PINHOLE, K=[[80, 0, W / 2], [0, 80, H / 2], [0, 0, 1]], width=W, height=H,
-                            depth_min=2.0, depth_max=9.0)
+    if model == types.SPHERE:
+        cam = types.make_camera(types.SPHERE, params=[W / (2 * math.pi), W / 2, H / 2], width=W, height=H,
+                                depth_min=2.0, depth_max=9.0)
+    else:
+        cam = types.make_camera(types.PINHOLE, K=[[80, 0, W / 2], [0, 80, H / 2], [0, 0, 1]], width=W, height=H,
+                                depth_min=2.0, depth_max=9.0)
     rng = np.random.default_rng(5)
     depths = rng.uniform(3, 6, (H, W)).astype(np.float32)
     costs = rng.uniform(0, 0.3, (H, W)).astype(np.float32)
@@ -255,3 +262,23 @@ def test_divide_and_conquer_delaunay(monkeypatch, layout, threads):
     if layout == "general":
         monkeypatch.setenv("ACMMP_DELAUNAY_INCREMENTAL", "1")
         np.testing.assert_array_equal(capi.delaunay(pts, W, H), tri)
+
+
+def test_concurrent_delaunay_calls_share_the_host_pool():
+    """Several contexts' planar blocks triangulate at once (the pipeline's overlapped planar passes) on the one
+    process-wide host worker pool (planar_prior.cpp HostPool): every concurrent call's triangles equal its serial
+    result."""
+    from concurrent.futures import ThreadPoolExecutor
+    rng = np.random.default_rng(23)
+    cases = []
+    for k in range(4):
+        W, H = 800 + 200 * k, 600 + 100 * k
+        pts = np.array([(c + rng.integers(0, 5), r + rng.integers(0, 5)) for c in range(0, W, 5) for r in range(0, H, 5)
+                        if rng.random() < 0.35 + 0.1 * k], np.int32)
+        cases.append((pts, W, H))
+    serial = [capi.delaunay(p, W, H) for p, W, H in cases]
+    with ThreadPoolExecutor(4) as ex:
+        futs = [ex.submit(capi.delaunay, p, W, H) for _ in range(3) for p, W, H in cases]
+        got = [f.result() for f in futs]
+    for k, g in enumerate(got):
+        np.testing.assert_array_equal(g, serial[k % len(cases)])
