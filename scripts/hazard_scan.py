@@ -8,10 +8,19 @@ f16_fma_lo, ...) scheduled right after the producer read a half-written register
 wrong values (round 6: k_eval_ref's paired-sample loop, max_abs of a v_sqrt result).  This scan flags every
 (producer, next instruction) pair that reads the producer's result with no instruction in between.
 
-usage: python scripts/hazard_scan.py file.s [...]     (hipcc --cuda-device-only -S output); exit 1 on a hit
+usage: python scripts/hazard_scan.py file.s [...]     (hipcc --cuda-device-only -S output)
+       python scripts/hazard_scan.py --so libacmmp.so    (the built library: its gfx950 code objects unbundled
+                                                          and disassembled with the image's llvm-objdump)
+exit 1 on a hit.
 """
+import os
 import re
+import shutil
+import subprocess
 import sys
+import tempfile
+
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 TRANS = re.compile(r"^\s*(v_(?:rcp|rcp_iflag|sqrt|rsq|exp|log|sin|cos)_f(?:32|16)(?:_e32|_e64)?)\s+(v\d+)")
 INSTR = re.compile(r"^\s*([a-z_][a-z0-9_]*)\b(.*)$")
@@ -26,13 +35,28 @@ def regs(operands):
     return out
 
 
-def scan(path):
+def disassemble_so(so):
+    """The gfx950 code objects of a HIP shared library, disassembled -> list of (name, text)."""
+    out = []
+    with tempfile.TemporaryDirectory() as td:
+        lib = os.path.join(td, "lib.so")
+        shutil.copyfile(so, lib)
+        subprocess.run([OBJDUMP, "--offloading", lib], check=True, capture_output=True, cwd=td)
+        for f in sorted(os.listdir(td)):
+            if "gfx950" in f:
+                r = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", "--no-leading-addr", os.path.join(td, f)],
+                                   check=True, capture_output=True, text=True)
+                out.append((f, r.stdout))
+    return out
+
+
+def scan(path, text=None):
     hits = []
-    lines = open(path).read().split("\n")
+    lines = (open(path).read() if text is None else text).split("\n")
     fn = "?"
     for i, line in enumerate(lines):
-        if re.match(r"^_Z\w+:", line):
-            fn = line.split(":")[0]
+        if re.match(r"^_Z\w+:", line) or re.match(r"^_Z\w+>:", line.lstrip("<")):
+            fn = line.split(":")[0].strip("<>")
         m = TRANS.match(line)
         if not m:
             continue
@@ -45,6 +69,7 @@ def scan(path):
                 continue
             if not s or s.startswith(";") or s.startswith("."):
                 continue
+            s = s.split("//")[0].strip()
             im = INSTR.match(s)
             if not im:
                 break
@@ -56,10 +81,20 @@ def scan(path):
     return hits
 
 
+def scan_so(so):
+    hits = []
+    for name, text in disassemble_so(so):
+        hits += scan(name, text)
+    return hits
+
+
 if __name__ == "__main__":
     allhits = []
-    for p in sys.argv[1:]:
-        allhits += scan(p)
+    if sys.argv[1:2] == ["--so"]:
+        allhits = scan_so(sys.argv[2])
+    else:
+        for p in sys.argv[1:]:
+            allhits += scan(p)
     for h in allhits:
         print(f"{h[0]}:{h[1]} {'(inline asm) ' if h[5] else ''}{h[3]}  ->  {h[4]}   [{h[2][:90]}]")
     print(f"{len(allhits)} trans -> immediate-use pairs")
