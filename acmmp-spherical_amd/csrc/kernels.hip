@@ -349,9 +349,9 @@ __device__ __forceinline__ void sphere_pixel_fast(Cam& c, f32x2 t, float tz, flo
 // Two directions at once, their two atan polynomials as interleaved packed chains (a chain of dependent
 // v_pk_fma_f32 waits a hazard cycle between steps, s_nop; two chains fill each other's), the same operations per
 // direction as sphere_pixel_fast, so the same bits
-template <typename CamA, typename CamB>
-__device__ __forceinline__ void sphere_pixel_fast_x2(CamA& ca, f32x2 ta, float tza, CamB& cb, f32x2 tb, float tzb,
-                                                     float& oxa, float& oya, float& oxb, float& oyb) {
+template <typename Cam>
+__device__ __forceinline__ void sphere_pixel_fast_x2(Cam& c, f32x2 ta, float tza, f32x2 tb, float tzb, float& oxa,
+                                                     float& oya, float& oxb, float& oyb) {
     const float ha = __builtin_amdgcn_sqrtf(fmaf(tza, tza, ta.x * ta.x));
     const float hb = __builtin_amdgcn_sqrtf(fmaf(tzb, tzb, tb.x * tb.x));
     const f32x2 mna = (f32x2){min_abs_nt(tza, ta.x), min_abs_h(ha, ta.y)};
@@ -384,8 +384,8 @@ __device__ __forceinline__ void sphere_pixel_fast_x2(CamA& ca, f32x2 ta, float t
     rb.x = __builtin_bit_cast(int, tzb) < 0 ? kPiHi - rb.x : rb.x;
     const f32x2 anga = (f32x2){copysignf(ra.x, ta.x), copysignf(ra.y, ta.y)};
     const f32x2 angb = (f32x2){copysignf(rb.x, tb.x), copysignf(rb.y, tb.y)};
-    const f32x2 oa = pk_fma(anga, (f32x2){ca.fkx, ca.fky}, (f32x2){ca.cx, ca.cy});
-    const f32x2 ob = pk_fma(angb, (f32x2){cb.fkx, cb.fky}, (f32x2){cb.cx, cb.cy});
+    const f32x2 oa = pk_fma(anga, (f32x2){c.fkx, c.fky}, (f32x2){c.cx, c.cy});
+    const f32x2 ob = pk_fma(angb, (f32x2){c.fkx, c.fky}, (f32x2){c.cx, c.cy});
     oxa = oa.x; oya = oa.y; oxb = ob.x; oyb = ob.y;
 }
 
@@ -758,14 +758,6 @@ __device__ __forceinline__ void sphere_fold_sample(float w, float r, float sp, f
 //    through a pointer instead took k_eval_ref from 120 to 256 VGPRs.)
 // With kFixNone every sample is projected.
 constexpr uint32_t kFixNone = ~0u, kFixNan = ~0u - 1u;
-// the interpolation nodes through the plane's homography (ncc_chunk; 0 builds round 5's ray-plane depth + rigid
-// map per node for A/Bs)
-#ifndef ACMMP_NODE_HOMOG
-#define ACMMP_NODE_HOMOG 1
-#endif
-#ifndef ACMMP_NODE_PAIRS
-#define ACMMP_NODE_PAIRS 1
-#endif
 
 // The lane's index in its wave, read where it is used: an asm volatile statement is neither hoisted nor merged
 // with another read, so a value derived from it is not kept live from the prologue (k_eval_nb spilled its lane
@@ -900,7 +892,6 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
             constexpr int kNode[4] = {0, 2, 3, 5};
             const float spread_max = kp.spread_max;     // source pixels spanned by the corner nodes (see below)
             uint32_t rough = 0u;                        // views whose nodes spread too far (below)
-#if ACMMP_NODE_HOMOG
             // A node's source direction through the plane's homography (round 6): the node's point in the
             // reference frame is d r with d = -w / (n . r), so its source-frame point is
             //     t = d FR r + Ft = d (FR - Ft n^T / w) r = d M r,
@@ -927,14 +918,12 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 if (!(emax <= -1e-6f) || ph.w == 0.0f) rough = 0xffffffffu;
             }
             const float kw = -__builtin_amdgcn_rcpf(ph.w);   // -1 / w
-#endif
 #pragma unroll
             for (int v = 0; v < VB; ++v) {
                 if (!has(v)) continue;
                 ConstCam& c = PCV(v);
                 const __amdgpu_buffer_rsrc_t rs =
                     __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(c.img16_base), 0, c.img16_bytes, 0x00020000);
-#if ACMMP_NODE_HOMOG
                 // M = FR - Ft n^T / w, rows 0 and 1 interleaved per column as FRxy is
                 f32x2 Mxy[3];
                 float Mz[3];
@@ -949,7 +938,6 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         Mz[k] = fmaf(fkz, n3[k], c.FRz[k]);
                     }
                 }
-#endif
                 float x00 = 0.f;                            // the first node's x (set below)
                 // one patch column's six samples from its four row nodes (x, y): the bilinear tap and the
                 // sums of ACMMP.cu:488-498
@@ -1039,7 +1027,6 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         }
                         nd[b].y = y;
                     };
-#if ACMMP_NODE_HOMOG && ACMMP_NODE_PAIRS
                     // two nodes at a time: their atan polynomials interleave (a lone chain of dependent v_pk_fma_f32
                     // waits a hazard cycle between steps: 929 s_nop in k_eval_nb<11,4,1,1>, 348 paired; the same
                     // bits, scripts/ab_bitident.py)
@@ -1055,27 +1042,10 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                             hz[k] = fmaf(Mz[2], q.y, fmaf(Mz[1], rwy, Mz[0] * q.x));
                         }
                         float x0, y0, x1, y1;
-                        sphere_pixel_fast_x2(c, hxy[0], hz[0], c, hxy[1], hz[1], x0, y0, x1, y1);
+                        sphere_pixel_fast_x2(c, hxy[0], hz[0], hxy[1], hz[1], x0, y0, x1, y1);
                         put_node(b, x0, y0);
                         put_node(b + 1, x1, y1);
                     }
-#else
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        const float4 q = pt.rw[(kNode[a] * 6 + kNode[b]) * pt.stride];
-                        const float4 rw = make_float4(q.x, pt.rr[kNode[b] * pt.stride], q.y, q.z);
-                        float x, y;
-#if ACMMP_NODE_HOMOG
-                        const f32x2 hxy = pk_fma(Mxy[2], splat2(rw.z), pk_fma(Mxy[1], splat2(rw.y), Mxy[0] * splat2(rw.x)));
-                        const float hz = fmaf(Mz[2], rw.z, fmaf(Mz[1], rw.y, Mz[0] * rw.x));
-                        sphere_pixel_fast(c, hxy, hz, x, y);
-#else
-                        const float dep = depth_from_plane_fast(ph, rw);
-                        project_fast<MODEL>(c, make_float3(rw.x * dep, rw.y * dep, rw.z * dep), x, y);
-#endif
-                        put_node(b, x, y);
-                    }
-#endif
                     if (a == 0) {
                         x03 = nd[3].x;
                         y0max = fmaxf(nd[0].y, nd[3].y);
