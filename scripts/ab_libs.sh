@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round 6: bit-identity of two builds (scripts/ab_bitident.py), then alternated bench lines of variants, then the
-# product's planar-prior timing and end-to-end line.  Usage: bash scripts/r06_ab5.sh TAG BASE CAND "LIBS" "CONFIG1" ...
+# A/B of library builds on the GPU box: bit-identity of BASE and CAND (scripts/ab_bitident.py), alternated bench lines
+# of every library in LIBS (ACMMP_LIB selects one; scripts/build_variants.py builds them), then the product's planar-prior
+# timing and end-to-end line.  Usage: bash scripts/ab_libs.sh TAG BASE CAND "LIBS" "CONFIG1" ...   (CONFIG "" = metric)
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; BASE=$2; CAND=$3; LIBS=$4; shift 4
