@@ -1144,11 +1144,16 @@ acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx* c, uint64_t seed, int n_half_swe
         HIP_TRY(c, hipEventCreate(&e));
         c->kev.push_back(e);
     }
+    // per-kernel events: the k_eval_nb bucket always (the bench's roofline prices it); the other three buckets with
+    // ACMMP_KERNEL_TIMING=all in the environment (read per run) -- an event record between two kernels leaves the
+    // GPU idle ~6 us, 3 x 6 per half-sweep (0.6% of the metric's RunPatchMatch, profiles/r06_ab9_events_ab.txt)
+    const char* e_kt = std::getenv("ACMMP_KERNEL_TIMING");
+    const bool time_all = e_kt && std::strcmp(e_kt, "all") == 0;
     HIP_TRY(c, hipEventRecord(c->ev[1], s));
     for (int sw = 0; sw < n_half_sweeps; ++sw) {
         const int colour = sw & 1, iter = sw / 2;
         SweepOut out{c->d_plane_cs[colour][cur[colour] ^ 1], c->d_cost_cs[colour][cur[colour] ^ 1]};
-        HIP_TRY(c, launch_propagate(kp, colour, iter, out, s, &c->kev[5 * sw]));
+        HIP_TRY(c, launch_propagate(kp, colour, iter, out, s, &c->kev[5 * sw], time_all));
         cur[colour] ^= 1;
         kp.plane_cs[colour] = c->d_plane_cs[colour][cur[colour]];
         kp.cost_cs[colour] = c->d_cost_cs[colour][cur[colour]];
@@ -1175,9 +1180,9 @@ acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx* c, uint64_t seed, int n_half_swe
         c->work_total = 0;
         for (int sw = 0; sw < n_half_sweeps; ++sw) c->work_total += colour_pixels(c, kp, sw & 1);
     }
-    for (int k = 0; k < 4; ++k) { c->ktiming[k] = 0.f; c->klaunch[k] = n_half_sweeps; }
+    for (int k = 0; k < 4; ++k) { c->ktiming[k] = 0.f; c->klaunch[k] = k == 0 || time_all ? n_half_sweeps : 0; }
     for (int sw = 0; sw < n_half_sweeps; ++sw)
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < (time_all ? 4 : 1); ++k) {
             float ms = 0.f;
             HIP_TRY(c, hipEventElapsedTime(&ms, c->kev[5 * sw + k], c->kev[5 * sw + k + 1]));
             c->ktiming[k] += ms;

@@ -177,9 +177,10 @@ struct SweepOut {
 hipError_t launch_ray_tables(const KParams& kp, float4* dirs, float2* sph_row, float2* sph_col, hipStream_t s);
 hipError_t launch_spatial_table(const KParams& kp, float* spatial, hipStream_t s);
 hipError_t launch_init(const KParams& kp, hipStream_t s);
-// ev: null, or 5 events recorded around the 4 kernels of the half-sweep (per-kernel timing)
+// ev: null, or 5 events recorded around the 4 kernels of the half-sweep (per-kernel timing); all_marks false
+// records ev[0] and ev[1] only (the k_eval_nb bucket): each event record in the stream costs ~6 us of idle GPU
 hipError_t launch_propagate(const KParams& kp, int colour, int iter, SweepOut out, hipStream_t s,
-                            hipEvent_t* ev = nullptr);
+                            hipEvent_t* ev = nullptr, bool all_marks = true);
 hipError_t launch_post(const KParams& kp, int do_post, hipStream_t s);
 // Reference Camera -> device camera (derived constants computed as DESIGN.md §2.3 says), capi.cpp.
 DevCam make_devcam(const acmmp_camera& cam);

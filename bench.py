@@ -750,10 +750,10 @@ def main():
         "short_circuited_pixel_frac": round(1.0 - work[0] / max(work[1], 1), 4),
         "hbm": hbm,
         "executed": executed,
-        "half_sweep_kernels_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items()},
+        "half_sweep_kernels_ms": {k: round(v[0] / v[1], 4) for k, v in kern.items() if v[1]},  # k_eval_nb; all four
+        # with ACMMP_KERNEL_TIMING=all
         "half_sweep_reference_flop_tflops": round(algorithmic_flop_per_pixel(args.model, args.n_src) *
-                                                  pix_per_launch / (sum(v[0] for v in kern.values()) /
-                                                                    max(nb_n, 1) * 1e-3) / 1e12, 3),
+                                                  pix_per_launch / (stage[1] / max(nb_n, 1) * 1e-3) / 1e12, 3),
         "note": "FP32 vector peak (equal to the f32 MFMA dense peak); the path has no GEMM-shaped work",
     }
 

@@ -201,11 +201,13 @@ acmmp_status acmmp_synchronize(acmmp_ctx *ctx);
  * the kernels run on: [init, propagation (all half-sweeps), post]. */
 acmmp_status acmmp_last_timing(const acmmp_ctx *ctx, float ms[3]);
 
-/* Per-kernel device time of the last run's half-sweeps (HIP events around every launch, on the
+/* Per-kernel device time of the last run's half-sweeps (HIP events around the launches, on the
  * kernels' stream): summed ms and launch count for [k_eval_nb, k_select, k_eval_ref, k_finish]
  * (the stages one CheckerboardPropagation half-sweep is split into).  The k_eval_ref
  * bucket includes its tail launch (k_eval_ref_tail); the neighbour pick (k_pick) runs before the
- * k_eval_nb bucket opens and is in the propagation stage time only. */
+ * k_eval_nb bucket opens and is in the propagation stage time only.  Only the k_eval_nb bucket is
+ * timed unless ACMMP_KERNEL_TIMING=all was set in the environment for the run (each event record
+ * idles the GPU a few microseconds); an untimed bucket reports 0 ms over 0 launches. */
 acmmp_status acmmp_last_kernel_timing(const acmmp_ctx *ctx, float ms[4], int launches[4]);
 
 /* Work accounting of the last run's k_eval_nb launches: pixels whose NCCs were evaluated, and all

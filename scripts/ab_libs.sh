@@ -4,6 +4,7 @@
 # timing and end-to-end line.  Usage: bash scripts/ab_libs.sh TAG BASE CAND "LIBS" "CONFIG1" ...   (CONFIG "" = metric)
 set -o pipefail
 export TMPDIR=/tmp
+export ACMMP_KERNEL_TIMING=all   # every half-sweep bucket timed (the same event overhead in every library's line)
 TAG=$1; BASE=$2; CAND=$3; LIBS=$4; shift 4
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 ACMMP_LIB=$BASE timeout -k 10 300 python scripts/ab_bitident.py run $OUT/base.npz > $OUT/bit.log 2>&1 || { tail $OUT/bit.log; exit 1; }
