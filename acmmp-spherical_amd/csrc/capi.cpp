@@ -1146,7 +1146,7 @@ acmmp_status acmmp_run_patchmatch_ex(acmmp_ctx* c, uint64_t seed, int n_half_swe
     }
     // per-kernel events: the k_eval_nb bucket always (the bench's roofline prices it); the other three buckets with
     // ACMMP_KERNEL_TIMING=all in the environment (read per run) -- an event record between two kernels leaves the
-    // GPU idle ~6 us, 3 x 6 per half-sweep (0.6% of the metric's RunPatchMatch, profiles/r06_ab9_events_ab.txt)
+    // GPU idle ~6 us, 3 x 6 per half-sweep (0.45% of the metric's RunPatchMatch, profiles/r06_ab9_events_ab.txt)
     const char* e_kt = std::getenv("ACMMP_KERNEL_TIMING");
     const bool time_all = e_kt && std::strcmp(e_kt, "all") == 0;
     HIP_TRY(c, hipEventRecord(c->ev[1], s));

@@ -1987,6 +1987,10 @@ constexpr int ref_vb_eval() {
 __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour) {
     const long long q = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
     const int d = blockIdx.y;
+    // the fallback queue's region counters emptied for k_eval_nb's first view chunk (in place of a memset launch
+    // between this kernel and k_eval_nb: 4 us of GPU time per half-sweep)
+    static_assert(kNbFixRegions == 256, "one counter per thread of block (0, 0)");
+    if (kp.nbfix && blockIdx.x == 0 && d == 0) kp.nbfix_count[threadIdx.x] = 0u;
     int px = 0, py = 0;
     if (!colour_pixel(kp, colour, q, px, py)) return;
     const long long ci = static_cast<long long>(py) * kp.Wh + (px >> 1);
@@ -2146,6 +2150,10 @@ __global__ __launch_bounds__(256) void k_nb_fix(const KParams kp, const int colo
 template <int MODEL, int VB, bool GEOM>
 __global__ __launch_bounds__(256, ACMMP_SELECT_WAVES) void k_select(const KParams kp, const int colour, const int iter) {
     const long long q = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+    // k_eval_ref's per-block survivor counters, emptied here for the launch that follows (launch_eval_ref's grid:
+    // one per kRefPix of the npix work items this grid covers; in place of a memset launch)
+    if (kp.ref_split > 0 && q < (static_cast<long long>(kp.row_hi - kp.row_lo) * kp.Wh + kRefPix - 1) / kRefPix)
+        kp.surv_count[q] = 0u;
     int px = 0, py = 0;
     if (!colour_pixel(kp, colour, q, px, py)) return;
     const int V = kp.V;
@@ -3251,7 +3259,8 @@ hipError_t launch_eval_nb(const KParams& kp0, int colour, hipStream_t s) {
         // the queue holds one launch's entries (a region's lanes x the chunk's views): emptied before and
         // drained after every view chunk
         hipError_t e = hipSuccess;
-        if (fix && (e = hipMemsetAsync(kp.nbfix_count, 0, sizeof(unsigned) * kNbFixRegions, s)) != hipSuccess) return e;
+        // (k_pick empties them for the first chunk)
+        if (fix && v0 > 0 && (e = hipMemsetAsync(kp.nbfix_count, 0, sizeof(unsigned) * kNbFixRegions, s)) != hipSuccess) return e;
         if ((e = launch_eval_nb_views(kp, colour, s)) != hipSuccess) return e;
         if (fix) {
             k_nb_fix<1><<<16 * kNbFixRegions, 256, 0, s>>>(kp, colour);   // 16 stripes per region
@@ -3366,7 +3375,7 @@ hipError_t launch_eval_ref(const KParams& kp0, int colour, hipStream_t s) {
                                                                        : nb_lds_bytes(kp.model, kp.S, kp.nside, kRefPix);
     hipError_t e = hipSuccess;
     const dim3 grd_ref = static_cast<unsigned>(cdiv(npix, kRefPix));
-    if (kp.ref_split > 0 && (e = hipMemsetAsync(kp.surv_count, 0, sizeof(unsigned) * grd_ref.x, s)) != hipSuccess) return e;
+    // (surv_count[0 .. grd_ref.x) is emptied by k_select, which runs right before)
     // the interpolated instance (fast SPHERE, V > 4) queues its survivors' fallback views on k_eval_nb's queue
     // (drained by then): a region's k_eval_ref blocks x 255 candidates x S views fit its room (Pc S / 51 against
     // k_eval_nb's Pc x chunk / 32, S <= chunk)
