@@ -88,6 +88,7 @@ struct acmmp_ctx {
     float* d_spatial = nullptr;
 
     float4* d_planes_rm = nullptr;
+    float* d_w_rm = nullptr;                    // the post stage's depth channel (k_merge -> k_filter)
     float* d_costs_rm = nullptr;
     float* d_pre = nullptr;
     uint32_t* d_sel_rm = nullptr;
@@ -308,7 +309,7 @@ void acmmp_destroy(acmmp_ctx* c) {
     dfree(c->d_cams); dfree(c->d_img); dfree(c->d_img16); dfree(c->d_dep); dfree(c->d_dirs);
     dfree(c->d_stage); dfree(c->d_flag);
     dfree(c->d_sph_row); dfree(c->d_sph_col); dfree(c->d_spatial);
-    dfree(c->d_planes_rm); dfree(c->d_costs_rm); dfree(c->d_pre); dfree(c->d_sel_rm);
+    dfree(c->d_planes_rm); dfree(c->d_w_rm); dfree(c->d_costs_rm); dfree(c->d_pre); dfree(c->d_sel_rm);
     dfree(c->d_scaled); dfree(c->d_prior); dfree(c->d_mask); dfree(c->d_pp); dfree(c->d_support); dfree(c->d_scratch); dfree(c->d_work);
     for (int k = 0; k < 2; ++k) {
         for (int b = 0; b < 2; ++b) { dfree(c->d_plane_cs[k][b]); dfree(c->d_cost_cs[k][b]); }
@@ -652,6 +653,7 @@ static acmmp_status upload_views_impl(acmmp_ctx* c, int n, const float* const* i
         const size_t P = P_of(c);
         const size_t Pc = static_cast<size_t>(c->H) * Wh_of(c);
         HIP_TRY(c, dalloc(c->d_planes_rm, P));
+        HIP_TRY(c, dalloc(c->d_w_rm, P));
         HIP_TRY(c, dalloc(c->d_costs_rm, P));
         HIP_TRY(c, dalloc(c->d_pre, P));
         HIP_TRY(c, dalloc(c->d_sel_rm, P));
@@ -1086,7 +1088,7 @@ static acmmp_status build_kparams(acmmp_ctx* c, KParams& kp, uint64_t seed) {
     kp.sph_row = c->d_sph_row;
     kp.sph_col = c->d_sph_col;
     kp.spatial = c->d_spatial;
-    kp.planes_rm = c->d_planes_rm; kp.costs_rm = c->d_costs_rm; kp.pre_rm = c->d_pre; kp.sel_rm = c->d_sel_rm;
+    kp.planes_rm = c->d_planes_rm; kp.w_rm = c->d_w_rm; kp.costs_rm = c->d_costs_rm; kp.pre_rm = c->d_pre; kp.sel_rm = c->d_sel_rm;
     kp.scaled = c->d_scaled; kp.prior = c->d_prior; kp.mask = c->d_mask;
     for (int k = 0; k < 2; ++k) {
         kp.plane_cs[k] = c->d_plane_cs[k][0];

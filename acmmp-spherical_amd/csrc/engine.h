@@ -112,6 +112,7 @@ struct KParams {
     const float* spatial;           // [(SPHERE ? H : 1)][S]: -dist / (2 sigma_s^2) (ACMMP.cu:398-403)
     float color_den;                // 2 * sigma_color^2
     float4* planes_rm;              // persistent row-major state
+    float* w_rm;                    // planes_rm's .w (depth) as its own array: k_merge -> k_filter's taps (post only)
     float* costs_rm;
     float* pre_rm;
     uint32_t* sel_rm;

@@ -2910,6 +2910,7 @@ __global__ void k_merge(const KParams kp, const int do_post) {
         ph = to_world(kp.cams[0], ph);
     }
     kp.planes_rm[center] = ph;
+    if (do_post) kp.w_rm[center] = ph.w;                    // k_filter's taps (4-byte loads, not float4 lanes)
     kp.costs_rm[center] = kp.cost_cs[colour][ci];
     kp.sel_rm[center] = kp.sel_cs[colour][ci];
 }
@@ -2951,9 +2952,13 @@ __global__ void k_filter(const KParams kp, const int colour) {
     if (py >= kp.filt_hi[colour] || px >= kp.W) return;
     const int width = kp.W, height = kp.H;
     const long long center = static_cast<long long>(py) * width + px;
-    if (kp.costs_rm[center] < 0.001f) return;
-    const float4* P = kp.planes_rm;
-    auto wv = [&](long long i) { return P[i].w; };
+    const float cost = kp.costs_rm[center];                 // (tested after an interior pixel's taps are issued)
+    // the taps from k_merge's copy of the depth channel: a wave's 21 tap loads then span 8-byte strides instead of
+    // the float4 rows' 32 (every other pixel of a row per lane); the result goes to both (the red pass reads the
+    // black pass's results, ACMMP.cu:1549-1552)
+    const float* P = kp.w_rm;
+    auto wv = [&](long long i) { return P[i]; };
+    auto put = [&](float m) { kp.planes_rm[center].w = m; kp.w_rm[center] = m; };
     const int width_ = kp.W, height_ = kp.H;
     if (py > 4 && py < height_ - 5 && px > 4 && px < width_ - 5) {
         // interior: all 21 taps exist; the same insertion sort, unrolled over registers (the
@@ -2964,11 +2969,12 @@ __global__ void k_filter(const KParams kp, const int colour) {
                        wv(center + 1), wv(center + 3), wv(center + 5), wv(center - w + 2), wv(center + w + 2),
                        wv(center - w - 2), wv(center + w - 2), wv(center - 1 - 2 * w), wv(center + 1 - 2 * w),
                        wv(center - 1 + 2 * w), wv(center + 1 + 2 * w)};
+        if (cost < 0.001f) return;                           // ACMMP.cu:1397; the taps' loads already in flight
         bool plain = true;                                   // no NaN, no signed zero among the taps
 #pragma unroll
         for (int i = 0; i < 21; ++i) plain = plain && d[i] == d[i] && d[i] != 0.0f;
         if (plain) {
-            kp.planes_rm[center].w = median21(d);
+            put(median21(d));
             return;
         }
 #pragma unroll
@@ -2984,9 +2990,10 @@ __global__ void k_filter(const KParams kp, const int colour) {
             }
             if (moving) d[0] = tmp;
         }
-        kp.planes_rm[center].w = d[10];
+        put(d[10]);
         return;
     }
+    if (cost < 0.001f) return;
     // border pixels: the taps that exist, in the reference's order (ACMMP.cu:1366-1450), insertion-sorted as sort_small
     // does -- in registers: each tap k is inserted into the sorted first n (<= k) with the interior's "still moving" flag
     // and the slots past n left alone, and the median read by a select over the slots.  (A private array indexed by the
@@ -3028,7 +3035,7 @@ __global__ void k_filter(const KParams kp, const int colour) {
         if (k == mi) hi = v[k];
     }
     const float med = (n % 2 == 0) ? (lo + hi) / 2 : hi;
-    kp.planes_rm[center].w = med;
+    put(med);
 }
 
 // JBU_cu, ACMMP.cu:1558-1616
