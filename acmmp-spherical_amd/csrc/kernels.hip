@@ -945,11 +945,13 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 // weights, so each term is one v_pk_fma_f32 (the same fma order per coordinate as the
                 // scalar chains, so the same bits)
 #ifndef ACMMP_COL_GROUP
-#define ACMMP_COL_GROUP 2
+#define ACMMP_COL_GROUP 6
 #endif
                 // the samples in groups of ACMMP_COL_GROUP: the group's texel loads issued before any of its
                 // sums (one sample at a time, the interpolated columns' loads were each waited for before the
-                // next issued); the sums still run in sample order, so the same bits
+                // next issued); the sums still run in sample order, so the same bits.  Round 6: the whole column
+                // (6 loads in flight; 92 -> 96 VGPRs, 2 spilled) against round 5's pairs: k_eval_nb 1.414 -> 1.396 ms,
+                // metric +0.5%, C3 +0.4%; groups of 3 lost 1.3% (profiles/r06_ab15_colgroup_ab.txt)
                 auto column = [&](int ci, const f32x2 (&nd)[4]) {
                     asm volatile("" ::: "memory");
                     // (k_eval_nb's instances only, NB: k_eval_ref's interpolating instance measured 1.3% slower)
