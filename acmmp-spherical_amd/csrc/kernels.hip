@@ -1122,6 +1122,13 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
     // the depth division and the point per sample) and no FR in scalar registers across the loop; in
     // binary32 emulation (C5 / C2 cameras, near-surface planes) the coordinates are ~2x closer to float64
     // than the per-sample form's (q99 8e-5 vs 1.7e-4 px).
+// fast pinhole sample loop: two samples' loads in flight (ACMMP_PIN_PAIRS: k_eval_nb's, _REF: k_eval_ref's instances)
+#ifndef ACMMP_PIN_PAIRS
+#define ACMMP_PIN_PAIRS 1
+#endif
+#ifndef ACMMP_PIN_PAIRS_REF
+#define ACMMP_PIN_PAIRS_REF 1
+#endif
     constexpr bool kHomog = FM && MODEL == kPinhole && STAGED == 3;
     if constexpr (kHomog) if (kp.homog) {
         interp_done = 1;
@@ -1193,19 +1200,18 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                 nr[v] = pk_fma(splat2(fi), hi2[v], n0[v]);
                 zr[v] = fmaf(fi, hiz[v], z0[v]);
             }
-            for (int j = -R; j <= R; j += inc, ++s) {
-                const float fj = static_cast<float>(j);
-                const float4 q = pt.rw[s * pt.stride];      // (r_s, w_s)
-                const float r = pt.rr[s * pt.stride];
+            // one sample's source points and texel loads (its sums after)
+            auto issue = [&](int jv, int sv, Tap (&tp)[VB], bool (&okv)[VB], float& w_o, float& r_o, f32x2& wwr_o) {
+                const float fj = static_cast<float>(jv);
+                const float4 q = pt.rw[sv * pt.stride];     // (r_s, w_s)
+                r_o = pt.rr[sv * pt.stride];
                 const float D = dot3(ph.x, ph.y, ph.z, q.x, q.y, q.z);
                 const float dS = (fabsf(D) < 1e-6f ? w_clamp : -D) - s0;
-                const float w = q.w;
-                const f32x2 wwr = (f32x2){w, w * r};
-                Tap tap[VB];
-                bool ok[VB];
+                w_o = q.w;
+                wwr_o = (f32x2){w_o, w_o * r_o};
 #pragma unroll
                 for (int v = 0; v < VB; ++v) {
-                    ok[v] = false;
+                    okv[v] = false;
                     if (has(v)) {
                         f32x2 nn = pk_fma(splat2(fj), hj2[v], nr[v]);
                         float tz = fmaf(fj, hjz[v], zr[v]);
@@ -1213,11 +1219,40 @@ __device__ __forceinline__ void ncc_chunk(const KParams& kp, int px, int py, con
                         tz = fmaf(dS, ftz[v], tz);
                         const f32x2 o = pk_fma(nn, splat2(__builtin_amdgcn_rcpf(tz)), xy0[v]);
                         const int ix = cvt_flr_i32(o.x), iy = cvt_flr_i32(o.y);
-                        ok[v] = (static_cast<unsigned>(ix) <= static_cast<unsigned>(wm1[v])) &
-                                (static_cast<unsigned>(iy) <= static_cast<unsigned>(hm1[v]));   // pin_in_image
-                        tap[v] = fetch_tap_pin_p<TEX>(rsv[v], p4[v], o.x, o.y, ix, iy);
+                        okv[v] = (static_cast<unsigned>(ix) <= static_cast<unsigned>(wm1[v])) &
+                                 (static_cast<unsigned>(iy) <= static_cast<unsigned>(hm1[v]));   // pin_in_image
+                        tp[v] = fetch_tap_pin_p<TEX>(rsv[v], p4[v], o.x, o.y, ix, iy);
                     }
                 }
+            };
+            int j = -R;
+            if constexpr (NB ? ACMMP_PIN_PAIRS : ACMMP_PIN_PAIRS_REF) {
+                // k_eval_nb: two samples' loads in flight before either's sums (the sums in sample order, so the
+                // same bits).  Round 6, at the 5-wave budget (96 VGPRs, 2 spilled; 44 spilled at 6 waves): C2 k_eval_nb
+                // 3.05 -> 2.93 ms, C2 +2.3%, 1920x1080 V=20 +1.8% (profiles/r06_ab17_pinpairs_ab.txt); in k_eval_ref's
+                // fast pinhole chunks (100 -> 117 VGPRs, 5 -> 4 waves) C2 k_eval_ref 1.78 -> 1.71 ms, C2 +1.6% more
+                // (profiles/r06_ab18_pinpairs_ref_ab.txt)
+                for (; j + inc <= R; j += 2 * inc, s += 2) {
+                    Tap ta[VB], tb[VB];
+                    bool oka[VB], okb[VB];
+                    float wa, ra, wb, rb;
+                    f32x2 wwra, wwrb;
+                    issue(j, s, ta, oka, wa, ra, wwra);
+                    issue(j + inc, s + 1, tb, okb, wb, rb, wwrb);
+#pragma unroll
+                    for (int v = 0; v < VB; ++v)
+                        if (has(v)) ACMMP_ACCUMULATE_T(v, ta[v], wa, wwra, ra, oka[v]);
+#pragma unroll
+                    for (int v = 0; v < VB; ++v)
+                        if (has(v)) ACMMP_ACCUMULATE_T(v, tb[v], wb, wwrb, rb, okb[v]);
+                }
+            }
+            for (; j <= R; j += inc, ++s) {
+                Tap tap[VB];
+                bool ok[VB];
+                float w, r;
+                f32x2 wwr;
+                issue(j, s, tap, ok, w, r, wwr);
 #pragma unroll
                 for (int v = 0; v < VB; ++v)
                     if (has(v)) ACMMP_ACCUMULATE(v);
@@ -2009,10 +2044,12 @@ __global__ __launch_bounds__(256) void k_pick(const KParams kp, const int colour
 // fast pinhole: 6 waves (80 VGPRs, 5 dwords spilled outside the sample loops) against 5 unconstrained (90):
 // C2 k_eval_nb 3.233 -> 3.212 ms (profiles/r04_ab5_ab.txt).  A software-pipelined form of its sample loop (the
 // next sample's gathers issued before the current one is accumulated: 96 VGPRs, 5 waves) measured 3.17 -> 3.30 ms
-// (round 5, profiles/r05_ab3_ab.txt): not kept.
+// (round 5, profiles/r05_ab3_ab.txt): not kept.  Round 6: two samples' loads issued before either's sums (the sums
+// in order, not a pipeline across iterations) at 5 waves (96 VGPRs, 2 spilled) -- C2 k_eval_nb 3.05 -> 2.93 ms
+// (profiles/r06_ab17_pinpairs_ab.txt); at 6 waves the pair spilled 44 dwords.
 template <int MODEL, int VB, int TEX, int FM>
 #ifndef ACMMP_NB_PIN_WAVES
-#define ACMMP_NB_PIN_WAVES 6
+#define ACMMP_NB_PIN_WAVES 5
 #endif
 #ifndef ACMMP_NB_SPH_WAVES
 // fast SPHERE: 5 waves (92 VGPRs, no spills).  Round 4's form (all 16 nodes of a view live at once) spilled 9 dwords at
